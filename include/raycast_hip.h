@@ -1,0 +1,184 @@
+/*
+ * raycast_hip.h — C-ABI of the MI355X raycast library (libraycast_hip.so).
+ *
+ * Drop-in boundary: the reference's render entry point
+ *     void raycast(json_data_t *json_struct, PPMFormat photo_data);   // C/raycast.h:8
+ * is exported with the identical signature and by-value PPMFormat, so the reference's
+ * own main (C/raycast.c:19-69) links against this library instead of C/raycast.c.
+ *
+ * The record layouts below are byte-identical to the reference's:
+ *   shape_t  (104 B)  C/objects.h:15-49
+ *   light_t  ( 72 B)  C/objects.h:51-61
+ *   json_data_t       C/parse.h:11-18
+ *   PPMFormat         C/ppm.h:6-12
+ * They sit behind the reference's own include guards (objects_h, parse_h, ppm_h): include
+ * the reference headers FIRST if both are used in one translation unit.
+ *
+ * Everything beyond raycast() is an extension: explicit options (mode, bounce depth, GPU
+ * count), a reusable packed scene, and device-resident rendering for benchmarks and the
+ * multi-GPU driver.  No torch types cross this boundary: plain pointers and sizes only.
+ */
+#ifndef RAYCAST_HIP_H
+#define RAYCAST_HIP_H
+
+#include <stdio.h>
+#include <stdint.h>
+#include <stdbool.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- reference record layouts (ABI) ------------------------------------------------- */
+#ifndef objects_h
+#define objects_h
+typedef enum { SPHERE, PLANE, QUADRIC } shape_type_t;        /* C/objects.h:4-8   */
+typedef enum { POINT, SPOTLIGHT } light_type_t;               /* C/objects.h:10-13 */
+
+typedef struct shape_t {                                      /* C/objects.h:15-49 */
+  float diffuse_color[3];
+  float specular_color[3];
+  float position[3];
+  float reflectivity;
+  float refractivity;
+  float ior;
+  union {
+    struct { float normal[3]; };                              /* plane   */
+    struct { float radius; };                                 /* sphere  */
+    struct { float a, b, c, d, e, f, g, h, i, j; };           /* quadric */
+  };
+  shape_type_t type;
+  struct shape_t *next;
+} shape_t;
+
+typedef struct light_t {                                      /* C/objects.h:51-61 */
+  float position[3];
+  float color[3];
+  float radial_coef[3];
+  float theta;
+  float cos_theta;
+  float a0;
+  float direction[3];
+  light_type_t type;
+  struct light_t *next;
+} light_t;
+
+/* list builders of the host front end (same names/semantics as C/objects.c:20-221) */
+shape_t *add_new_sphere(shape_t *head, float *diffuse, float *specular, float *position,
+                        float radius, float reflectivity, float refractivity, float ior);
+shape_t *add_new_plane(shape_t *head, float *diffuse, float *specular, float *position,
+                       float *normal, float reflectivity);
+shape_t *add_new_quadric(shape_t *head, float *diffuse, float *specular, float a, float b,
+                         float c, float d, float e, float f, float g, float h, float i,
+                         float j, float reflectivity);
+shape_t *free_shape_list(shape_t *head);
+light_t *free_light_list(light_t *head);
+light_t *add_new_spot_light(light_t *head, float *color, float *position, float theta,
+                            float a0, float *direction, float *radial_coef);
+light_t *add_new_point_light(light_t *head, float *color, float *position, float *radial_coef);
+#endif
+
+#ifndef parse_h
+#define parse_h
+typedef struct json_data_t {                                  /* C/parse.h:11-18 */
+  float camera_width;
+  float camera_height;
+  shape_t *shapes_list;
+  light_t *lights_list;
+  int num_shapes;
+  int num_lights;
+} json_data_t;
+
+/* scene front end (same grammar, messages and exit(1) behaviour as C/parse.c:13-436) */
+void parse_json(FILE *json, json_data_t *json_data);
+void set_to_black(float *input);
+#endif
+
+#ifndef ppm_h
+#define ppm_h
+typedef struct PPMFormat {                                    /* C/ppm.h:6-12 */
+  int width, height, size;
+  uint8_t maxColor;
+  uint8_t depth;
+  char *tupleType;
+  uint8_t *pixmap;
+} PPMFormat;
+
+void ppm_WriteOutP3(PPMFormat inData, FILE *outFile);        /* C/ppm.c:168-184 */
+float ppm_clamp(float value, float lower_bound, float upper_bound);  /* C/ppm.c:350-359 */
+#endif
+
+_Static_assert(sizeof(shape_t) == 104, "shape_t must match C/objects.h layout");
+_Static_assert(sizeof(light_t) == 72, "light_t must match C/objects.h layout");
+
+/* ---- drop-in entry point ------------------------------------------------------------ */
+
+/* Replaces C/raycast.c:79-130.  Consumes both lists exactly like the reference
+ * (C/raycast.c:104-107: frees them; num_shapes/num_lights stay valid; the list pointers are
+ * left NULL instead of dangling).  Writes every byte of photo_data.pixmap (W*H*3, RGB,
+ * row-major, top row first).  Options come from the environment:
+ *   RAYCAST_MODE   = parity (default) | fast
+ *   RAYCAST_DEPTH  = bounce depth d, MAX_RECURSION = d+1 (default 6 == C/raycast.c:14)
+ *   RAYCAST_GPUS   = number of GPUs for row-cyclic sharding (default 1)
+ *   RAYCAST_DEVICE = first HIP device ordinal (default 0)
+ *   RAYCAST_STATS  = 1: one JSON metrics line on stderr
+ * Any HIP failure prints a message to stderr and exit(1)s (reference error convention). */
+void raycast(json_data_t *json_struct, PPMFormat photo_data);
+
+/* ---- extended API ------------------------------------------------------------------- */
+
+enum { RC_MODE_PARITY = 0,  /* byte-identical to gcc -O3 C/raycast.c (scan-order carry)   */
+       RC_MODE_FAST   = 1   /* reflection miss ends the bounce loop (CUDA/raycast.cu:224-237) */ };
+
+typedef struct rc_options {
+  int max_recursion;   /* C/raycast.c:14 MAX_RECURSION; bounce depth = max_recursion - 1 */
+  int mode;            /* RC_MODE_* */
+  int num_gpus;        /* >= 1 */
+  int device;          /* first device ordinal */
+} rc_options;
+
+typedef struct rc_timing {
+  double total_ms;       /* whole call, host wall clock                                 */
+  double kernel_ms;      /* sum of kernel spans (HIP events)                            */
+  double resolve_ms;     /* parity: carry-chain resolution span                        */
+  double d2h_ms;         /* device -> host copy of the pixmap                          */
+  int64_t dep_pixels;    /* parity: pixels whose first reflection missed               */
+  int64_t zero_normalize;/* count of zero-length normalize events (C/v3math.c:183-187) */
+} rc_timing;
+
+/* Fill *opt with the defaults (then the RAYCAST_* environment overrides if use_env). */
+void rc_default_options(rc_options *opt, int use_env);
+
+/* Opaque packed scene: flattened shape/light arrays + the out-of-bounds "phantom" record
+ * the reference reads as shapes_list[-1] (C/raycast.c:382).  Does NOT consume the lists. */
+typedef struct rc_scene rc_scene;
+rc_scene *rc_scene_create(const json_data_t *json_struct);
+void rc_scene_destroy(rc_scene *scene);
+/* 1 when the reference output is well defined for this scene (phantom reads only defined
+ * bytes or is black), 0 when the reference itself is run-to-run nondeterministic. */
+int rc_scene_parity_defined(const rc_scene *scene);
+
+/* Render W x H into a host pixmap (W*H*3 bytes).  Returns 0 on success. */
+int rc_render(const rc_scene *scene, int width, int height, const rc_options *opt,
+              uint8_t *pixmap, rc_timing *timing);
+
+/* Device-resident render on the current device: rows row0, row0+row_step, ... (nrows rows)
+ * of a W x H image into d_out (nrows*W*3 bytes, device memory, compact row order) on the
+ * given HIP stream (NULL = default stream).  Parity mode requires row0=0,row_step=1,nrows=H.
+ * Asynchronous except for the parity resolver's host handshake.  Returns 0 on success. */
+int rc_render_device(const rc_scene *scene, int width, int height, int row0, int row_step,
+                     int nrows, const rc_options *opt, uint8_t *d_out, void *stream,
+                     rc_timing *timing);
+
+/* Average duration (ms) of the last rc_render_device() call's main shading kernel,
+ * measured with HIP events on its stream. */
+double rc_last_kernel_ms(void);
+
+/* Library version / build string. */
+const char *rc_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RAYCAST_HIP_H */
