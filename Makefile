@@ -1,0 +1,62 @@
+# Build of the MI355X raycaster (gfx950) — everything in-tree.
+#
+#   make            libraycast_hip.so (HIP kernels + C-ABI), libraycast_front.so (host
+#                   scene parser / P3 writer), bin/raytrace (drop-in CLI), oracle
+#   make ref        oracle/_ref: the reference C/ sources compiled in place (test oracle)
+#
+# Numerics flags (parity with the x86-64 gcc -O3 reference):
+#   -ffp-contract=off                    no a*b+c fusion (hipcc defaults to fast-honor-pragmas)
+#   -fno-gpu-flush-denormals-to-zero     f32 denormals kept, like SSE2
+#   -fhip-fp32-correctly-rounded-divide-sqrt   IEEE f32 division
+# Host C: gcc -O3 without -march (no FMA), like C/Makefile:4.
+
+HIPCC   ?= /opt/rocm/bin/hipcc
+CC      ?= gcc
+PKG     := raytracing-programs_amd
+SRC     := $(PKG)/csrc
+LIB     := $(PKG)/lib
+BIN     := $(PKG)/bin
+OBJ     := $(PKG)/lib/obj
+ARCH    ?= gfx950
+
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off \
+            -fno-gpu-flush-denormals-to-zero -fhip-fp32-correctly-rounded-divide-sqrt \
+            -Iinclude -I$(SRC) -Wall -Wno-gnu-anonymous-struct -Wno-nested-anon-types \
+            -Wno-c11-extensions -Wno-unused-result
+CFLAGS   := -O3 -ffp-contract=off -fPIC -Wall -Wno-unused-result -Iinclude -I$(SRC)
+
+HIP_SRCS  := $(SRC)/rc_kernels.hip $(SRC)/rc_api.hip
+HIP_HDRS  := $(SRC)/rc_device.hpp $(SRC)/rc_kernels.h $(SRC)/rc_scene.h include/raycast_hip.h
+FRONT_SRC := $(SRC)/front/parse.c $(SRC)/front/objects.c $(SRC)/front/ppm.c
+
+.PHONY: all oracle ref clean
+all: $(LIB)/libraycast_hip.so $(LIB)/libraycast_front.so $(BIN)/raytrace oracle
+
+$(OBJ)/%.o: $(SRC)/%.hip $(HIP_HDRS)
+	@mkdir -p $(OBJ)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(OBJ)/rc_scene.o: $(SRC)/rc_scene.c $(SRC)/rc_scene.h include/raycast_hip.h
+	@mkdir -p $(OBJ)
+	$(CC) $(CFLAGS) -c $< -o $@
+
+$(LIB)/libraycast_hip.so: $(OBJ)/rc_kernels.o $(OBJ)/rc_api.o $(OBJ)/rc_scene.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -o $@ -lpthread
+
+$(LIB)/libraycast_front.so: $(FRONT_SRC) include/raycast_hip.h
+	@mkdir -p $(LIB)
+	$(CC) $(CFLAGS) -shared $(FRONT_SRC) -o $@ -lm
+
+$(BIN)/raytrace: $(SRC)/front/raytrace_main.c $(LIB)/libraycast_front.so $(LIB)/libraycast_hip.so
+	@mkdir -p $(BIN)
+	$(CC) $(CFLAGS) $< -L$(LIB) -lraycast_front -lraycast_hip -Wl,-rpath,'$$ORIGIN/../lib' -o $@
+
+oracle:
+	$(MAKE) -C oracle oracle
+
+ref:
+	$(MAKE) -C oracle ref
+
+clean:
+	rm -rf $(LIB) $(BIN)
+	$(MAKE) -C oracle clean

@@ -1,0 +1,252 @@
+"""raytracing-programs_amd — Python host bindings of the MI355X raycaster.
+
+The product is C: ``lib/libraycast_hip.so`` (HIP kernels + the C-ABI declared in
+``include/raycast_hip.h``) and ``lib/libraycast_front.so`` (scene parser / P3 writer with the
+reference's names and behaviour, C/parse.c, C/objects.c, C/ppm.c).  This module only binds
+them with ctypes so tests and ``bench.py`` can drive the same entry points the C CLI uses:
+
+    scene = Scene.from_file("tests/golden/scenes/quadric.scene")   # parse_json (C/parse.c:13)
+    img = render(scene, 4096, 4096, depth=6, mode="parity")       # raycast (C/raycast.h:8)
+
+There is no CPU fallback: loading fails loudly if the shared libraries are missing, and a
+render fails if no GPU is present.  Import name: ``raytracing_programs_amd`` (the directory
+name has a hyphen; ``__graft_entry__`` and tests load it by path).
+"""
+import ctypes
+import os
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_DIR = os.path.join(PKG_DIR, "lib")
+BIN_DIR = os.path.join(PKG_DIR, "bin")
+ROOT_DIR = os.path.dirname(PKG_DIR)
+
+MODE_PARITY = 0
+MODE_FAST = 1
+MODES = {"parity": MODE_PARITY, "fast": MODE_FAST}
+
+
+# ------------------------------------------------------------------ ABI structs --
+class ShapeT(ctypes.Structure):
+    """shape_t, C/objects.h:15-49 (104 bytes)."""
+    _fields_ = [("diffuse_color", ctypes.c_float * 3), ("specular_color", ctypes.c_float * 3),
+                ("position", ctypes.c_float * 3), ("reflectivity", ctypes.c_float),
+                ("refractivity", ctypes.c_float), ("ior", ctypes.c_float),
+                ("u", ctypes.c_float * 10), ("type", ctypes.c_int),
+                ("next", ctypes.c_void_p)]
+
+
+class LightT(ctypes.Structure):
+    """light_t, C/objects.h:51-61 (72 bytes)."""
+    _fields_ = [("position", ctypes.c_float * 3), ("color", ctypes.c_float * 3),
+                ("radial_coef", ctypes.c_float * 3), ("theta", ctypes.c_float),
+                ("cos_theta", ctypes.c_float), ("a0", ctypes.c_float),
+                ("direction", ctypes.c_float * 3), ("type", ctypes.c_int),
+                ("next", ctypes.c_void_p)]
+
+
+class JsonDataT(ctypes.Structure):
+    """json_data_t, C/parse.h:11-18."""
+    _fields_ = [("camera_width", ctypes.c_float), ("camera_height", ctypes.c_float),
+                ("shapes_list", ctypes.POINTER(ShapeT)), ("lights_list", ctypes.POINTER(LightT)),
+                ("num_shapes", ctypes.c_int), ("num_lights", ctypes.c_int)]
+
+
+class RcOptions(ctypes.Structure):
+    _fields_ = [("max_recursion", ctypes.c_int), ("mode", ctypes.c_int),
+                ("num_gpus", ctypes.c_int), ("device", ctypes.c_int)]
+
+
+class RcTiming(ctypes.Structure):
+    _fields_ = [("total_ms", ctypes.c_double), ("kernel_ms", ctypes.c_double),
+                ("resolve_ms", ctypes.c_double), ("d2h_ms", ctypes.c_double),
+                ("dep_pixels", ctypes.c_int64), ("zero_normalize", ctypes.c_int64)]
+
+
+assert ctypes.sizeof(ShapeT) == 104 and ctypes.sizeof(LightT) == 72
+
+# the functions include/raycast_hip.h declares, per library
+HIP_EXPORTS = ["raycast", "rc_default_options", "rc_scene_create", "rc_scene_destroy",
+               "rc_scene_parity_defined", "rc_render", "rc_render_device", "rc_last_kernel_ms",
+               "rc_version"]
+FRONT_EXPORTS = ["add_new_sphere", "add_new_plane", "add_new_quadric", "free_shape_list",
+                 "free_light_list", "add_new_spot_light", "add_new_point_light", "parse_json",
+                 "set_to_black", "ppm_WriteOutP3", "ppm_clamp"]
+
+_libs = {}
+
+
+def _load(name):
+    if name not in _libs:
+        path = os.path.join(LIB_DIR, name)
+        if not os.path.exists(path):
+            raise RuntimeError(f"{path} is missing: build with `make` (or __graft_entry__.build())")
+        _libs[name] = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+    return _libs[name]
+
+
+def front_lib():
+    lib = _load("libraycast_front.so")
+    lib.parse_json.argtypes = [ctypes.c_void_p, ctypes.POINTER(JsonDataT)]
+    lib.parse_json.restype = None
+    lib.free_shape_list.argtypes = [ctypes.c_void_p]
+    lib.free_shape_list.restype = ctypes.c_void_p
+    lib.free_light_list.argtypes = [ctypes.c_void_p]
+    lib.free_light_list.restype = ctypes.c_void_p
+    return lib
+
+
+def hip_lib():
+    lib = _load("libraycast_hip.so")
+    lib.rc_scene_create.argtypes = [ctypes.POINTER(JsonDataT)]
+    lib.rc_scene_create.restype = ctypes.c_void_p
+    lib.rc_scene_destroy.argtypes = [ctypes.c_void_p]
+    lib.rc_scene_parity_defined.argtypes = [ctypes.c_void_p]
+    lib.rc_render.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                              ctypes.POINTER(RcOptions), ctypes.c_void_p, ctypes.POINTER(RcTiming)]
+    lib.rc_render_device.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                     ctypes.c_int, ctypes.c_int, ctypes.POINTER(RcOptions),
+                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(RcTiming)]
+    lib.rc_last_kernel_ms.restype = ctypes.c_double
+    lib.rc_version.restype = ctypes.c_char_p
+    lib.rc_default_options.argtypes = [ctypes.POINTER(RcOptions), ctypes.c_int]
+    return lib
+
+
+_libc = ctypes.CDLL(None)
+_libc.fopen.restype = ctypes.c_void_p
+_libc.fopen.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+_libc.fclose.argtypes = [ctypes.c_void_p]
+
+
+class Scene:
+    """A parsed scene: the reference's json_data_t lists plus the packed device scene."""
+
+    def __init__(self, js):
+        self.js = js
+        self._packed = None
+
+    @classmethod
+    def from_file(cls, path):
+        """parse_json (C/parse.c:13) through libraycast_front.so.  Like the reference, a
+        malformed file makes the parser print to stderr and exit(1)."""
+        lib = front_lib()
+        f = _libc.fopen(os.fsencode(path), b"r")
+        if not f:
+            raise FileNotFoundError(path)
+        js = JsonDataT()
+        try:
+            lib.parse_json(f, ctypes.byref(js))
+        finally:
+            _libc.fclose(f)
+        return cls(js)
+
+    @property
+    def num_shapes(self):
+        return self.js.num_shapes
+
+    @property
+    def num_lights(self):
+        return self.js.num_lights
+
+    def shapes(self):
+        out, p = [], self.js.shapes_list
+        while p:
+            out.append(p.contents)
+            p = ctypes.cast(p.contents.next, ctypes.POINTER(ShapeT))
+        return out
+
+    def lights(self):
+        out, p = [], self.js.lights_list
+        while p:
+            out.append(p.contents)
+            p = ctypes.cast(p.contents.next, ctypes.POINTER(LightT))
+        return out
+
+    def packed(self):
+        """rc_scene handle (packed image + phantom record) for the HIP library."""
+        if self._packed is None:
+            h = hip_lib().rc_scene_create(ctypes.byref(self.js))
+            if not h:
+                raise RuntimeError("rc_scene_create failed")
+            self._packed = h
+        return self._packed
+
+    def parity_defined(self):
+        return bool(hip_lib().rc_scene_parity_defined(self.packed()))
+
+    def close(self):
+        if self._packed is not None:
+            hip_lib().rc_scene_destroy(self._packed)
+            self._packed = None
+        lib = front_lib()
+        if self.js.shapes_list:
+            lib.free_shape_list(ctypes.cast(self.js.shapes_list, ctypes.c_void_p))
+            self.js.shapes_list = None
+        if self.js.lights_list:
+            lib.free_light_list(ctypes.cast(self.js.lights_list, ctypes.c_void_p))
+            self.js.lights_list = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def options(depth=6, mode="parity", gpus=1, device=0):
+    opt = RcOptions()
+    opt.max_recursion = depth + 1
+    opt.mode = MODES[mode] if isinstance(mode, str) else int(mode)
+    opt.num_gpus = gpus
+    opt.device = device
+    return opt
+
+
+def render(scene, width, height, depth=6, mode="parity", gpus=1, device=0, timing=None):
+    """Render to a host array [H, W, 3] uint8 through rc_render (the raycast() path)."""
+    lib = hip_lib()
+    out = np.empty((height, width, 3), dtype=np.uint8)
+    t = RcTiming()
+    opt = options(depth, mode, gpus, device)
+    rc = lib.rc_render(scene.packed(), width, height, ctypes.byref(opt),
+                       out.ctypes.data_as(ctypes.c_void_p), ctypes.byref(t))
+    if rc != 0:
+        raise RuntimeError("rc_render failed (no GPU, or HIP error: see stderr)")
+    if timing is not None:
+        timing.update({k: getattr(t, k) for k, _ in RcTiming._fields_})
+    return out
+
+
+def render_device(scene, width, height, d_out_ptr, stream_ptr=None, depth=6, mode="parity",
+                  row0=0, row_step=1, nrows=None, timing=None):
+    """Render rows row0, row0+row_step, ... into device memory at d_out_ptr (nrows*W*3 B)."""
+    lib = hip_lib()
+    nrows = height if nrows is None else nrows
+    opt = options(depth, mode)
+    t = RcTiming()
+    rc = lib.rc_render_device(scene.packed(), width, height, row0, row_step, nrows,
+                              ctypes.byref(opt), ctypes.c_void_p(d_out_ptr),
+                              ctypes.c_void_p(stream_ptr or 0),
+                              ctypes.byref(t) if timing is not None else None)
+    if rc != 0:
+        raise RuntimeError("rc_render_device failed (see stderr)")
+    if timing is not None:
+        timing.update({k: getattr(t, k) for k, _ in RcTiming._fields_})
+
+
+def last_kernel_ms():
+    return hip_lib().rc_last_kernel_ms()
+
+
+def encode_p3(img):
+    """The reference P3 byte stream (C/ppm.c:168-184) of an [H, W, 3] uint8 image."""
+    h, w, _ = img.shape
+    table = [f"{v}\n".encode() for v in range(256)]
+    body = b"".join(table[v] for v in img.reshape(-1).tolist())
+    return f"P3\n{w} {h} \n255\n".encode() + body
+
+
+def version():
+    return hip_lib().rc_version().decode()

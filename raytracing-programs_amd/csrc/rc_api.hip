@@ -1,0 +1,417 @@
+// rc_api.hip — host runtime and C-ABI of libraycast_hip.so (declared in include/raycast_hip.h).
+//
+// raycast() is the drop-in for C/raycast.c:79-130: it flattens the lists (rc_scene.c),
+// consumes them like the reference (C/raycast.c:104-107), renders on the GPU(s) and writes
+// photo_data.pixmap.  Per-device state (stream, events, grow-only workspaces) is created on
+// first use and kept for the life of the process, so repeated renders allocate nothing.
+//
+// Multi-GPU inside one process (RAYCAST_GPUS=N, fast mode): one host thread per device,
+// rows dealt cyclically (row r -> device r mod N; contiguous blocks are 1.7-2.1x imbalanced,
+// SURVEY.md §5), each device renders its rows into a compact buffer and a strided 2-D copy
+// drops them straight into their interleaved place in the host pixmap.  The multi-process
+// (one rank per GPU, RCCL gather) path is driven from Python: see bench.py.
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "raycast_hip.h"
+#include "rc_kernels.h"
+#include "rc_scene.h"
+
+#define RC_VERSION "raycast-mi355x 0.1 (gfx950)"
+
+namespace {
+
+#define HIP_TRY(expr)                                                                   \
+  do {                                                                                  \
+    hipError_t e_ = (expr);                                                             \
+    if (e_ != hipSuccess) {                                                             \
+      std::fprintf(stderr, "Error: HIP call failed: %s (%s) at %s:%d\n", #expr,        \
+                   hipGetErrorString(e_), __FILE__, __LINE__);                          \
+      return -1;                                                                        \
+    }                                                                                   \
+  } while (0)
+
+constexpr int kMaxDevices = 16;
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  int ensure(size_t need) {
+    if (need <= bytes) return 0;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+    if (hipMalloc(&p, need) != hipSuccess) return -1;
+    bytes = need;
+    return 0;
+  }
+};
+
+struct DevCtx {
+  bool init = false;
+  int device = 0;
+  int cus = 256;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev[5] = {};
+  DevBuf out;          // rc_render output pixmap
+  DevBuf zcount;       // zero-normalize counter
+  DevBuf scene;        // uploaded packed scene
+  const void* scene_src = nullptr;   // host image last uploaded
+  // parity workspace
+  DevBuf cls, wcarry, deprec, rows, dep_pix, dep_key, seg_start, cin, counters;
+  size_t parity_pixels = 0;
+  int parity_rows = 0;
+};
+
+DevCtx g_ctx[kMaxDevices];
+std::mutex g_ctx_mu;
+double g_last_kernel_ms = 0.0;
+
+int ctx_get(int device, DevCtx** out) {
+  if (device < 0 || device >= kMaxDevices) return -1;
+  std::lock_guard<std::mutex> lk(g_ctx_mu);
+  DevCtx& c = g_ctx[device];
+  if (!c.init) {
+    HIP_TRY(hipSetDevice(device));
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, device));
+    c.cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    HIP_TRY(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
+    for (auto& e : c.ev) HIP_TRY(hipEventCreate(&e));
+    if (c.zcount.ensure(64)) return -1;
+    c.device = device;
+    c.init = true;
+  }
+  *out = &c;
+  return 0;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------- scene object --
+struct rc_scene {
+  rc_packed_header* img;   // host packed image
+};
+
+extern "C" {
+
+const char* rc_version(void) { return RC_VERSION; }
+
+double rc_last_kernel_ms(void) { return g_last_kernel_ms; }
+
+void rc_default_options(rc_options* opt, int use_env) {
+  opt->max_recursion = 7;   // C/raycast.c:14
+  opt->mode = RC_MODE_PARITY;
+  opt->num_gpus = 1;
+  opt->device = 0;
+  if (!use_env) return;
+  if (const char* m = std::getenv("RAYCAST_MODE")) {
+    if (!std::strcmp(m, "fast")) opt->mode = RC_MODE_FAST;
+    else if (!std::strcmp(m, "parity")) opt->mode = RC_MODE_PARITY;
+    else std::fprintf(stderr, "Warning: unknown RAYCAST_MODE '%s', using parity\n", m);
+  }
+  if (const char* d = std::getenv("RAYCAST_DEPTH")) opt->max_recursion = std::atoi(d) + 1;
+  if (const char* g = std::getenv("RAYCAST_GPUS")) opt->num_gpus = std::atoi(g);
+  if (const char* v = std::getenv("RAYCAST_DEVICE")) opt->device = std::atoi(v);
+  if (opt->num_gpus < 1) opt->num_gpus = 1;
+}
+
+rc_scene* rc_scene_create(const json_data_t* js) {
+  if (!js) return nullptr;
+  rc_packed_header* img = rc_pack_scene(js);
+  if (!img) return nullptr;
+  rc_scene* s = (rc_scene*)std::calloc(1, sizeof(rc_scene));
+  if (!s) {
+    std::free(img);
+    return nullptr;
+  }
+  s->img = img;
+  return s;
+}
+
+void rc_scene_destroy(rc_scene* s) {
+  if (!s) return;
+  // forget device copies that were uploaded from this image
+  for (auto& c : g_ctx)
+    if (c.scene_src == s->img) c.scene_src = nullptr;
+  std::free(s->img);
+  std::free(s);
+}
+
+int rc_scene_parity_defined(const rc_scene* s) { return s ? s->img->phantom_defined : 0; }
+
+}  // extern "C"
+
+namespace {
+
+int upload_scene(DevCtx& c, const rc_scene* s, rc::LaunchScene& ls) {
+  const rc_packed_header* h = s->img;
+  if (c.scene_src != h) {
+    if (c.scene.ensure((size_t)h->bytes)) return -1;
+    HIP_TRY(hipMemcpyAsync(c.scene.p, h, (size_t)h->bytes, hipMemcpyHostToDevice, c.stream));
+    c.scene_src = h;
+  }
+  const char* base = (const char*)c.scene.p;
+  ls.shapes = (const rc_shape*)(base + h->off_shapes);
+  ls.lights = (const rc_light*)(base + h->off_lights);
+  ls.pairs = (const rc_shade_pair*)(base + h->off_pairs);
+  ls.n = h->n;
+  ls.m = h->m;
+  ls.cam_w = h->cam_w;
+  ls.cam_h = h->cam_h;
+  return 0;
+}
+
+int ensure_parity(DevCtx& c, int W, int H, rc::ParityWork& w) {
+  const size_t P = (size_t)W * H;
+  if (c.cls.ensure(P) || c.wcarry.ensure(P * sizeof(float4)) ||
+      c.deprec.ensure(P * rc::deprec_bytes()) ||
+      c.rows.ensure((size_t)H * (2 * sizeof(int) + 4 * sizeof(long long)) + 256) ||
+      c.dep_pix.ensure(P * sizeof(long long)) || c.dep_key.ensure(P * sizeof(long long)) ||
+      c.seg_start.ensure(P * sizeof(int)) || c.cin.ensure(P * sizeof(float4)) ||
+      c.counters.ensure(64))
+    return -1;
+  char* r = (char*)c.rows.p;
+  w.cls = (uint8_t*)c.cls.p;
+  w.wcarry = (float4*)c.wcarry.p;
+  w.deprec = c.deprec.p;
+  w.row_lastw = (long long*)r;   r += (size_t)H * sizeof(long long);
+  w.row_lastdep = (long long*)r; r += (size_t)H * sizeof(long long);
+  w.row_prevw = (long long*)r;   r += (size_t)H * sizeof(long long);
+  w.row_prevdep = (long long*)r; r += (size_t)H * sizeof(long long);
+  w.row_ndep = (int*)r;          r += (size_t)H * sizeof(int);
+  w.row_off = (int*)r;
+  w.dep_pix = (long long*)c.dep_pix.p;
+  w.dep_key = (long long*)c.dep_key.p;
+  w.seg_start = (int*)c.seg_start.p;
+  w.cin = (float4*)c.cin.p;
+  w.counters = (int*)c.counters.p;
+  w.resolve_blocks = c.cus * 4;
+  w.phase_c_blocks = c.cus * 8;
+  return 0;
+}
+
+// Enqueue one render of rows (row0 + k*row_step) into d_out on c.stream.
+int enqueue_render(DevCtx& c, const rc_scene* s, int W, int H, int row0, int row_step, int nrows,
+                   const rc_options* opt, uint8_t* d_out, hipStream_t stream, bool timed) {
+  rc::LaunchScene ls;
+  if (upload_scene(c, s, ls)) return -1;
+  unsigned long long* zc = (unsigned long long*)c.zcount.p;
+  HIP_TRY(hipMemsetAsync(zc, 0, sizeof(unsigned long long), stream));
+  const int maxrec = opt->max_recursion;
+  const bool parity = opt->mode == RC_MODE_PARITY && maxrec > 1;
+  if (timed) HIP_TRY(hipEventRecord(c.ev[0], stream));
+  if (!parity) {
+    HIP_TRY(rc::launch_render(ls, W, H, row0, row_step, nrows, maxrec, d_out, zc, stream));
+    if (timed) HIP_TRY(hipEventRecord(c.ev[1], stream));
+    return 0;
+  }
+  if (row0 != 0 || row_step != 1 || nrows != H) {
+    std::fprintf(stderr, "Error: parity mode renders whole images only\n");
+    return -1;
+  }
+  rc::ParityWork w;
+  if (ensure_parity(c, W, H, w)) {
+    std::fprintf(stderr, "Error: out of device memory for the parity workspace\n");
+    return -1;
+  }
+  HIP_TRY(rc::launch_parity(ls, W, H, maxrec, d_out, w, zc, stream, timed ? c.ev[1] : nullptr,
+                            timed ? c.ev[2] : nullptr, timed ? c.ev[3] : nullptr));
+  return 0;
+}
+
+double event_ms(hipEvent_t a, hipEvent_t b) {
+  float ms = 0.0f;
+  if (hipEventElapsedTime(&ms, a, b) != hipSuccess) return 0.0;
+  return ms;
+}
+
+void fill_device_timing(DevCtx& c, const rc_options* opt, rc_timing* t) {
+  const bool parity = opt->mode == RC_MODE_PARITY && opt->max_recursion > 1;
+  double k = parity ? event_ms(c.ev[0], c.ev[3]) : event_ms(c.ev[0], c.ev[1]);
+  g_last_kernel_ms = parity ? event_ms(c.ev[0], c.ev[1]) : k;
+  if (!t) return;
+  t->kernel_ms = k;
+  t->resolve_ms = parity ? event_ms(c.ev[1], c.ev[2]) : 0.0;
+  unsigned long long z = 0;
+  if (hipMemcpy(&z, c.zcount.p, sizeof z, hipMemcpyDeviceToHost) == hipSuccess)
+    t->zero_normalize = (int64_t)z;
+  if (parity) {
+    int cnt[4] = {0, 0, 0, 0};
+    if (hipMemcpy(cnt, c.counters.p, sizeof cnt, hipMemcpyDeviceToHost) == hipSuccess)
+      t->dep_pixels = cnt[2];
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int rc_render_device(const rc_scene* s, int W, int H, int row0, int row_step, int nrows,
+                     const rc_options* opt, uint8_t* d_out, void* stream, rc_timing* timing) {
+  if (!s || !opt || !d_out || W <= 0 || H <= 0 || nrows < 0 || row_step < 1) return -1;
+  if (row0 < 0 || (nrows > 0 && row0 + (long long)(nrows - 1) * row_step >= H)) return -1;
+  if (nrows == 0) return 0;
+  int dev = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  DevCtx* c;
+  if (ctx_get(dev, &c)) return -1;
+  hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+  // the scene upload and events live on the ctx stream: order them with the caller's stream
+  if (st != c->stream) {
+    hipStream_t saved = c->stream;
+    c->stream = st;
+    int rc = enqueue_render(*c, s, W, H, row0, row_step, nrows, opt, d_out, st, true);
+    c->stream = saved;
+    if (rc) return rc;
+  } else if (enqueue_render(*c, s, W, H, row0, row_step, nrows, opt, d_out, st, true)) {
+    return -1;
+  }
+  if (timing) {
+    std::memset(timing, 0, sizeof *timing);
+    HIP_TRY(hipStreamSynchronize(st));
+    fill_device_timing(*c, opt, timing);
+    timing->total_ms = timing->kernel_ms;
+  }
+  return 0;
+}
+
+int rc_render(const rc_scene* s, int W, int H, const rc_options* opt, uint8_t* pixmap,
+              rc_timing* timing) {
+  if (!s || !opt || !pixmap || W <= 0 || H <= 0) return -1;
+  auto t0 = std::chrono::steady_clock::now();
+  if (timing) std::memset(timing, 0, sizeof *timing);
+  int ndev = 0;
+  HIP_TRY(hipGetDeviceCount(&ndev));
+  int G = opt->num_gpus;
+  if (opt->device < 0 || opt->device >= ndev) {
+    std::fprintf(stderr, "Error: device %d not available (%d devices)\n", opt->device, ndev);
+    return -1;
+  }
+  if (G > ndev - opt->device) G = ndev - opt->device;
+  if (G > H) G = H;
+  const bool parity = opt->mode == RC_MODE_PARITY && opt->max_recursion > 1;
+  if (parity) G = 1;   // the scan-order carry chain is resolved on one device
+  const size_t row_bytes = (size_t)W * 3;
+  std::vector<int> rcodes(G, 0);
+  std::vector<rc_timing> tims(G);
+  auto work = [&](int g) {
+    const int dev = opt->device + g;
+    DevCtx* c;
+    if (hipSetDevice(dev) != hipSuccess || ctx_get(dev, &c)) {
+      rcodes[g] = -1;
+      return;
+    }
+    const int nrows = (H - g + G - 1) / G;
+    if (nrows <= 0) return;
+    if (c->out.ensure((size_t)nrows * row_bytes)) {
+      rcodes[g] = -1;
+      return;
+    }
+    uint8_t* d_out = (uint8_t*)c->out.p;
+    if (enqueue_render(*c, s, W, H, g, G, nrows, opt, d_out, c->stream, true)) {
+      rcodes[g] = -1;
+      return;
+    }
+    auto td = std::chrono::steady_clock::now();
+    hipError_t e = hipMemcpy2DAsync(pixmap + (size_t)g * row_bytes, row_bytes * G, d_out,
+                                    row_bytes, row_bytes, nrows, hipMemcpyDeviceToHost,
+                                    c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) {
+      std::fprintf(stderr, "Error: HIP copy failed: %s\n", hipGetErrorString(e));
+      rcodes[g] = -1;
+      return;
+    }
+    std::memset(&tims[g], 0, sizeof(rc_timing));
+    fill_device_timing(*c, opt, &tims[g]);
+    tims[g].d2h_ms =
+        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - td).count();
+  };
+  if (G == 1) {
+    work(0);
+  } else {
+    std::vector<std::thread> th;
+    for (int g = 0; g < G; ++g) th.emplace_back(work, g);
+    for (auto& t : th) t.join();
+  }
+  for (int g = 0; g < G; ++g)
+    if (rcodes[g]) return -1;
+  if (timing) {
+    for (int g = 0; g < G; ++g) {
+      if (tims[g].kernel_ms > timing->kernel_ms) timing->kernel_ms = tims[g].kernel_ms;
+      if (tims[g].resolve_ms > timing->resolve_ms) timing->resolve_ms = tims[g].resolve_ms;
+      if (tims[g].d2h_ms > timing->d2h_ms) timing->d2h_ms = tims[g].d2h_ms;
+      timing->dep_pixels += tims[g].dep_pixels;
+      timing->zero_normalize += tims[g].zero_normalize;
+    }
+    timing->total_ms =
+        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  }
+  return 0;
+}
+
+static void consume_lists(json_data_t* js) {
+  for (shape_t* p = js->shapes_list; p;) {
+    shape_t* n = p->next;
+    std::free(p);
+    p = n;
+  }
+  for (light_t* p = js->lights_list; p;) {
+    light_t* n = p->next;
+    std::free(p);
+    p = n;
+  }
+  js->shapes_list = nullptr;
+  js->lights_list = nullptr;
+}
+
+// Drop-in for C/raycast.c:79-130.
+void raycast(json_data_t* json_struct, PPMFormat photo_data) {
+  rc_options opt;
+  rc_default_options(&opt, 1);
+  rc_scene* s = rc_scene_create(json_struct);
+  if (!s) {
+    std::fprintf(stderr, "Error: could not flatten the scene lists\n");
+    std::exit(1);
+  }
+  if (!rc_scene_parity_defined(s) && opt.mode == RC_MODE_PARITY)
+    std::fprintf(stderr,
+                 "Warning: the reference reads undefined memory for this scene "
+                 "(phantom record, C/raycast.c:382); its output is not reproducible\n");
+  // the reference consumes the lists (C/raycast.c:104-107)
+  consume_lists(json_struct);
+  if (photo_data.width <= 0 || photo_data.height <= 0) {   // the reference's loops do not run
+    rc_scene_destroy(s);
+    return;
+  }
+  rc_timing t;
+  if (rc_render(s, photo_data.width, photo_data.height, &opt, photo_data.pixmap, &t)) {
+    std::fprintf(stderr, "Error: GPU render failed\n");
+    std::exit(1);
+  }
+  // C/v3math.c:183-187 prints one line per zero-length normalize
+  for (int64_t k = 0; k < t.zero_normalize; ++k)
+    std::fprintf(stderr, "v3_length returned 0, exiting program\n");
+  if (const char* st = std::getenv("RAYCAST_STATS")) {
+    if (st[0] == '1')
+      std::fprintf(stderr,
+                   "{\"rays_per_s\": %.1f, \"total_ms\": %.3f, \"kernel_ms\": %.3f, "
+                   "\"resolve_ms\": %.3f, \"d2h_ms\": %.3f, \"dep_pixels\": %lld, "
+                   "\"mode\": \"%s\", \"gpus\": %d}\n",
+                   (double)photo_data.width * photo_data.height / (t.total_ms * 1e-3),
+                   t.total_ms, t.kernel_ms, t.resolve_ms, t.d2h_ms, (long long)t.dep_pixels,
+                   opt.mode == RC_MODE_FAST ? "fast" : "parity", opt.num_gpus);
+  }
+  rc_scene_destroy(s);
+}
+
+}  // extern "C"

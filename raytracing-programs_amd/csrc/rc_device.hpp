@@ -1,0 +1,458 @@
+// rc_device.hpp — per-pixel device routines of the MI355X raycaster.
+//
+// Bit-exact restatement of the reference render semantics (C/raycast.c:79-758,
+// C/v3math.c:19-192, C/ppm.c:350-359) for gfx950.  Compiled with -ffp-contract=off and
+// IEEE f32/f64 division and square root, so every float/double operation below rounds
+// exactly as the x86-64 gcc -O3 build does (SSE2, no FMA).  The two libm calls are replaced
+// by exact constructions:
+//   pow(x, 0.5)  -> sqrt(x)                         (byte-identical output)
+//   pow(x, 20)   -> x^20 in double-double, rounded once (correctly rounded)
+//   pow(a, n)    -> a^n in double-double for integer spot exponents
+//
+// Structure on CDNA4: one lane per pixel; the shape loop is wave-uniform (every lane tests
+// shape k together), so shape records are read with scalar loads into SGPRs and the
+// per-type branch is a scalar branch.  Hit post-processing (hit point, normal) is deferred
+// to after the loop: it depends only on (ray, t, shape), so computing it once for the final
+// winner is identical to the reference's write-on-every-accept (C/raycast.c:460-470).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rc_scene.h"
+
+namespace rc {
+
+constexpr int kModeFast = 0;      // reflection miss ends the bounce loop
+constexpr int kModeParityA = 1;   // parity, phase A: stop at a first-bounce miss (DEP pixel)
+constexpr int kModeParityC = 2;   // parity, phase C: first-bounce miss reads the given carry
+
+constexpr uint8_t kClsIdent = 0;  // pixel never writes the carry
+constexpr uint8_t kClsWriter = 1; // first bounce hit: carry-out independent of carry-in
+constexpr uint8_t kClsDep = 2;    // first bounce missed: needs the scan-order carry
+
+struct Scene {
+  const rc_shape* __restrict__ shapes;   // n + 1 records (n = phantom)
+  const rc_light* __restrict__ lights;   // m records
+  const rc_shade_pair* __restrict__ pairs;
+  int n, m;
+};
+
+struct Cam {
+  double hx, hy;   // (0.0 - cw/2.0) and (0.0 + ch/2.0)      C/raycast.c:115-116
+  float pw, ph;    // cw/(float)W, ch/(float)H                C/raycast.c:109-110
+};
+
+struct V3 {
+  float x, y, z;
+};
+
+__device__ __forceinline__ V3 v3(float x, float y, float z) { return V3{x, y, z}; }
+
+// C/v3math.c:69-71
+__device__ __forceinline__ float dot(V3 a, V3 b) {
+  float s = a.x * b.x;
+  s = s + a.y * b.y;
+  return s + a.z * b.z;
+}
+__device__ __forceinline__ V3 sub(V3 a, V3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
+
+// C/v3math.c:169-172 — (float)sqrt of an exact double sum of squares
+__device__ __forceinline__ float length(V3 a) {
+  double s = (double)a.x * (double)a.x;
+  s = s + (double)a.y * (double)a.y;
+  s = s + (double)a.z * (double)a.z;
+  return (float)__builtin_sqrt(s);
+}
+
+// C/v3math.c:180-192 — a zero length leaves the vector unchanged (and is counted: the
+// reference prints a stderr line per event)
+__device__ __forceinline__ V3 normalize(V3 a, int& zero_events) {
+  float len = length(a);
+  if (len == 0.0f) {
+    zero_events++;
+    return a;
+  }
+  return v3(a.x / len, a.y / len, a.z / len);
+}
+
+// C/v3math.c:144-160 — v - n*(2*dot(v,n))
+__device__ __forceinline__ V3 reflect(V3 v, V3 n) {
+  float s = 2.0f * dot(v, n);
+  return v3(v.x - n.x * s, v.y - n.y * s, v.z - n.z * s);
+}
+
+// ------------------------------------------------------------- double-double power --
+struct DD {
+  double hi, lo;
+};
+__device__ __forceinline__ DD dd_mul(DD a, DD b) {
+  double p = a.hi * b.hi;
+  double e = __builtin_fma(a.hi, b.hi, -p);
+  e = e + (a.hi * b.lo + a.lo * b.hi);
+  double s = p + e;
+  return DD{s, e - (s - p)};
+}
+__device__ __forceinline__ DD dd_from_prod(double a, double b) {
+  double p = a * b;
+  return DD{p, __builtin_fma(a, b, -p)};
+}
+__device__ __forceinline__ double dd_round(DD a) { return a.hi + a.lo; }
+
+// pow(x, 20) for the specular term (C/raycast.c:755-757); x = (double)float, so x*x is
+// exact in double and x^20 = (x^2)^8 * (x^2)^2 is built in double-double and rounded once.
+__device__ __forceinline__ double pow20(double x) {
+  double x2 = x * x;                  // exact: x has 24 significant bits
+  DD x4 = dd_from_prod(x2, x2);       // exact
+  DD x8 = dd_mul(x4, x4);
+  DD x16 = dd_mul(x8, x8);
+  DD x20 = dd_mul(x16, x4);
+  return dd_round(x20);
+}
+
+// pow(a, n) for an integer spot exponent (C/raycast.c:695), a = (double)float.
+__device__ __forceinline__ double pown_dd(double a, int n) {
+  if (n == 0) return 1.0;
+  unsigned e = n < 0 ? (unsigned)(-n) : (unsigned)n;
+  DD base{a, 0.0}, acc{1.0, 0.0};
+  while (e) {
+    if (e & 1u) acc = dd_mul(acc, base);
+    e >>= 1;
+    if (e) base = dd_mul(base, base);
+  }
+  if (n > 0) return dd_round(acc);
+  // 1 / acc in double-double, rounded once
+  double q = 1.0 / acc.hi;
+  DD qa = dd_mul(DD{q, 0.0}, acc);
+  double r = (1.0 - qa.hi) - qa.lo;
+  return q + q * r / 1.0;
+}
+
+// ------------------------------------------------------------------ intersections --
+// Per-ray sphere constants: `a` depends only on the ray direction (C/raycast.c:583), so it
+// is computed once per ray for every sphere test — the same value the reference recomputes.
+struct RayK {
+  float a4;     // 4 * a               (float, C/raycast.c:587)
+  double den;   // 2.0 * (double)a     (C/raycast.c:593)
+};
+__device__ __forceinline__ RayK ray_consts(V3 D) {
+  double aa = (double)D.x * (double)D.x;
+  aa = aa + (double)D.y * (double)D.y;
+  aa = aa + (double)D.z * (double)D.z;
+  float a = (float)aa;
+  return RayK{4.0f * a, 2.0 * (double)a};
+}
+
+// C/raycast.c:576-600
+__device__ __forceinline__ bool hit_sphere(V3 O, V3 D, const rc_shape& s, RayK k, float& t) {
+  V3 tv = v3(O.x - s.p[0], O.y - s.p[1], O.z - s.p[2]);
+  float b = 2.0f * dot(D, tv);
+  float c = (float)((double)dot(tv, tv) - s.r2);
+  float fac = k.a4 * c;
+  float disc = (float)((double)b * (double)b - (double)fac);
+  if (disc < 0.0f) return false;
+  double sq = __builtin_sqrt((double)disc);
+  float tt = (float)(((double)(-b) - sq) / k.den);
+  if (tt < 0.0f) tt = (float)(((double)(-b) + sq) / k.den);
+  t = tt;
+  return true;
+}
+
+// C/raycast.c:545-562
+__device__ __forceinline__ bool hit_plane(V3 O, V3 D, const rc_shape& s, float& t) {
+  V3 n = v3(s.n[0], s.n[1], s.n[2]);
+  float num = dot(v3(O.x - s.p[0], O.y - s.p[1], O.z - s.p[2]), n);
+  float den = dot(D, n);
+  if (den == 0.0f) return false;
+  float tt = (-num) / den;
+  if (tt < 0.0f) return false;
+  t = tt;
+  return true;
+}
+
+// C/raycast.c:614-656 — double accumulations in source order, float products as written
+__device__ __forceinline__ bool hit_quadric(V3 O, V3 D, const rc_shape& q, float& t) {
+  double acc;
+  acc = q.A * ((double)D.x * (double)D.x);
+  acc = acc + q.B * ((double)D.y * (double)D.y);
+  acc = acc + q.C * ((double)D.z * (double)D.z);
+  acc = acc + (double)(q.qd * D.x * D.y);
+  acc = acc + (double)(q.qe * D.x * D.z);
+  acc = acc + (double)(q.qf * D.y * D.z);
+  const float aq = (float)acc;
+
+  acc = 2.0 * q.A * (double)O.x * (double)D.x;
+  acc = acc + 2.0 * q.B * (double)O.y * (double)D.y;
+  acc = acc + 2.0 * q.C * (double)O.z * (double)D.z;
+  acc = acc + (double)(q.qd * (O.x * D.y + O.y * D.x));
+  acc = acc + (double)(q.qe * (O.x * D.z + O.z * D.x));
+  acc = acc + (double)(q.qf * (O.y * D.z + O.z * D.y));
+  acc = acc + (double)(q.qg * D.x);
+  acc = acc + (double)(q.qh * D.y);
+  acc = acc + (double)(q.qi * D.z);
+  const float bq = (float)acc;
+
+  acc = q.A * ((double)O.x * (double)O.x);
+  acc = acc + q.B * ((double)O.y * (double)O.y);
+  acc = acc + q.C * ((double)O.z * (double)O.z);
+  acc = acc + (double)(q.qd * O.x * O.y);
+  acc = acc + (double)(q.qe * O.x * O.z);
+  acc = acc + (double)(q.qf * O.y * O.z);
+  acc = acc + (double)(q.qg * O.x);
+  acc = acc + (double)(q.qh * O.y);
+  acc = acc + (double)(q.qi * O.z);
+  acc = acc + (double)q.qj;
+  const float cq = (float)acc;
+
+  if ((double)aq == 0.0) {
+    t = (float)((-1.0 * (double)cq) / (double)bq);
+    return true;
+  }
+  const float disc = (float)((double)bq * (double)bq - 4.0 * (double)aq * (double)cq);
+  if ((double)disc < 0.0) return false;
+  const double den = 2.0 * (double)aq;
+  const double sq = __builtin_sqrt((double)disc);
+  float tt = (float)(((double)(-bq) - sq) / den);
+  if (tt <= 0.0f) tt = (float)(((double)(-bq) + sq) / den);
+  t = tt;
+  return true;
+}
+
+// Shape test k for ray (O, D); `skip` is the bounce ray's skip index (-1 for primary and
+// shadow-from-phantom rays).  Returns whether the shape would be accepted as a candidate
+// with distance t (before the nearest/positive check).  Type is wave-uniform.
+__device__ __forceinline__ bool test_shape(const rc_shape& s, V3 O, V3 D, RayK rk, int skip,
+                                           float& t) {
+  const int type = s.type;
+  if (type == RC_SHAPE_SPHERE) return hit_sphere(O, D, s, rk, t);
+  if (type == RC_SHAPE_PLANE) return hit_plane(O, D, s, t);
+  if (type == RC_SHAPE_QUADRIC) {
+    if (!hit_quadric(O, D, s, t)) return false;
+    // C/raycast.c:492-494: for bounce rays a quadric hit below the origin's z is ignored
+    if (skip != -1 && (O.z + t * D.z) < O.z) return false;
+    return true;
+  }
+  return false;
+}
+
+// C/raycast.c:441-531 (shadow_test = false): index of the nearest accepted shape, its t.
+__device__ __forceinline__ int nearest(const Scene& sc, V3 O, V3 D, int skip, float& tbest) {
+  const RayK rk = ray_consts(D);
+  float best = __builtin_inff();
+  int idx = -1;
+  for (int k = 0; k < sc.n; ++k) {
+    float t = 0.0f;
+    const bool hit = test_shape(sc.shapes[k], O, D, rk, skip, t);
+    if (hit && k != skip && best > t && t > 0.0f) {
+      best = t;
+      idx = k;
+    }
+  }
+  tbest = best;
+  return idx;
+}
+
+// C/raycast.c:441-531 (shadow_test = true): is any shape hit with 0 < t < inf?  The first
+// such shape is always accepted, so the loop may stop there.
+__device__ __forceinline__ bool shadowed(const Scene& sc, V3 O, V3 D, int skip) {
+  const RayK rk = ray_consts(D);
+  for (int k = 0; k < sc.n; ++k) {
+    float t = 0.0f;
+    const bool hit = test_shape(sc.shapes[k], O, D, rk, skip, t);
+    if (hit && k != skip && __builtin_inff() > t && t > 0.0f) return true;
+  }
+  return false;
+}
+
+// Hit point and normal of the accepted shape (C/raycast.c:461-523).
+__device__ __forceinline__ void hit_frame(const Scene& sc, int idx, V3 O, V3 D, float t, V3& P,
+                                          V3& N, int& zero_events) {
+  P = v3(O.x + D.x * t, O.y + D.y * t, O.z + D.z * t);
+  const rc_shape& s = sc.shapes[idx];
+  const int type = s.type;
+  if (type == RC_SHAPE_SPHERE) {
+    const float inv = s.inv_r;
+    N = normalize(v3((P.x - s.p[0]) * inv, (P.y - s.p[1]) * inv, (P.z - s.p[2]) * inv),
+                  zero_events);
+  } else if (type == RC_SHAPE_PLANE) {
+    N = v3(s.n[0], s.n[1], s.n[2]);
+  } else {
+    double n0 = 2.0 * s.A * (double)P.x;
+    n0 = n0 + (double)(s.qd * P.y);
+    n0 = n0 + (double)(s.qe * P.z);
+    n0 = n0 + (double)s.qg;
+    double n1 = 2.0 * s.B * (double)P.y;
+    n1 = n1 + (double)(s.qd * P.x);
+    n1 = n1 + (double)(s.qf * P.z);
+    n1 = n1 + (double)s.qh;
+    double n2 = 2.0 * s.C * (double)P.z;
+    n2 = n2 + (double)(s.qe * P.x);
+    n2 = n2 + (double)(s.qf * P.y);
+    n2 = n2 + (double)s.qi;
+    N = normalize(v3((float)n0, (float)n1, (float)n2), zero_events);
+    if (dot(N, D) > 0.0f) N = v3(N.x * -1.0f, N.y * -1.0f, N.z * -1.0f);
+  }
+}
+
+// calc_color (C/raycast.c:381-421) for shape `idx` (sc.n = the phantom shapes_list[-1]).
+__device__ __forceinline__ V3 shade(const Scene& sc, int idx, V3 P, V3 N, V3 D, int& zero_events) {
+  const rc_shape& o = sc.shapes[idx];
+  const float opacity = o.opacity;
+  V3 out = v3(0.0f, 0.0f, 0.0f);
+  if (!(opacity > 0.0f)) return out;
+  const int skip = (idx == sc.n) ? -1 : idx;
+  const rc_shade_pair* pr = sc.pairs + (size_t)idx * sc.m;
+  for (int l = 0; l < sc.m; ++l) {
+    const rc_light& L = sc.lights[l];
+    V3 ld = v3(L.pos[0] - P.x, L.pos[1] - P.y, L.pos[2] - P.z);
+    const float dist = length(ld);
+    ld = normalize(ld, zero_events);
+    if (shadowed(sc, P, ld, skip)) continue;
+    // radial attenuation C/raycast.c:666-669
+    const float lin = L.r0 + L.r1 * dist;
+    const float rad =
+        (float)(1.0 / ((double)lin + (double)L.r2 * ((double)dist * (double)dist)));
+    // angular attenuation C/raycast.c:679-696
+    float ang = 1.0f;
+    if (L.type == RC_LIGHT_SPOT) {
+      V3 v = normalize(v3(P.x - L.pos[0], P.y - L.pos[1], P.z - L.pos[2]), zero_events);
+      const float alpha = dot(v, v3(L.dir[0], L.dir[1], L.dir[2]));
+      if (alpha < L.cos_theta) {
+        ang = 0.0f;
+      } else if (L.a0_kind == RC_A0_INT) {
+        ang = (float)pown_dd((double)alpha, L.a0_int);
+      } else {
+        ang = (float)pow((double)alpha, (double)L.a0);   // parity unpinned
+      }
+    }
+    // diffuse C/raycast.c:708-720, specular C/raycast.c:733-758
+    float dr = 0.0f, dg = 0.0f, db = 0.0f, sr = 0.0f, sg = 0.0f, sb = 0.0f;
+    const float th = dot(N, ld);
+    if (th > 0.0f) {
+      const rc_shade_pair& p = pr[l];
+      dr = p.dl[0] * th;
+      dg = p.dl[1] * th;
+      db = p.dl[2] * th;
+      const V3 view = v3(D.x * -1.0f, D.y * -1.0f, D.z * -1.0f);
+      const double angle = (double)dot(view, reflect(ld, N));
+      if (!(angle > 0.0)) {
+        const double p20 = pow20(angle);
+        sr = (float)((double)p.sl[0] * p20);
+        sg = (float)((double)p.sl[1] * p20);
+        sb = (float)((double)p.sl[2] * p20);
+      }
+    }
+    out.x = out.x + ((dr + sr) * rad) * ang;
+    out.y = out.y + ((dg + sg) * rad) * ang;
+    out.z = out.z + ((db + sb) * rad) * ang;
+  }
+  return v3(out.x * opacity, out.y * opacity, out.z * opacity);
+}
+
+// Primary ray of pixel (x, y) (C/raycast.c:115-118).
+__device__ __forceinline__ V3 primary_dir(const Cam& cam, int x, int y, int& zero_events) {
+  V3 d;
+  d.x = (float)(cam.hx + (double)cam.pw * ((double)x + 0.5));
+  d.y = (float)(cam.hy - (double)cam.ph * ((double)y + 0.5));
+  d.z = -1.0f;
+  return normalize(d, zero_events);
+}
+
+// ppm_clamp (C/ppm.c:350-359) + the float -> uint8_t store (C/raycast.c:122-126).
+// v_cvt_i32_f32 truncates and maps NaN to 0, like x86 cvttss2si's low byte.
+__device__ __forceinline__ uint8_t quant(float c) {
+  float v = c * 255.0f;
+  if (v > 255.0f) v = 255.0f;
+  if (v < 0.0f) v = 0.0f;
+  return (uint8_t)(int)v;
+}
+
+// State a first-bounce-miss (DEP) pixel carries from phase A to phases B/C.
+struct DepRec {
+  float d1x, d1y, d1z;   // reflected direction of the missed first bounce
+  float n0x, n0y, n0z;   // primary normal (misses never update the normal)
+  int obj0;              // primary shape (stale object of the loop, C/raycast.c:359-362)
+  int pad;
+};
+
+struct PixelOut {
+  V3 rgb;
+  uint8_t cls;
+  V3 carry;     // carry-out for writers (last bounce-hit point)
+  DepRec dep;
+};
+
+// iterative_shoot (C/raycast.c:315-379) for one pixel under MODE.
+//  kModeFast     : miss ends the loop.
+//  kModeParityA  : a miss at level 1 stops here (cls = DEP, dep record filled).
+//  kModeParityC  : `carry` is this pixel's scan-order carry-in.
+template <int MODE>
+__device__ __forceinline__ void shoot(const Scene& sc, V3 d, int maxrec, V3 carry, PixelOut& po,
+                                      int& zero_events) {
+  po.rgb = v3(0.0f, 0.0f, 0.0f);
+  po.cls = kClsIdent;
+  float t0;
+  const int i0 = nearest(sc, v3(0.0f, 0.0f, 0.0f), d, -1, t0);
+  if (i0 < 0) return;                                   // C/raycast.c:328-331
+  V3 P0, N0;
+  hit_frame(sc, i0, v3(0.0f, 0.0f, 0.0f), d, t0, P0, N0, zero_events);
+
+  int obj = i0, S = i0;
+  V3 O = P0, D = d, N = N0, C = carry;
+  float T = sc.shapes[i0].refl;
+  V3 out = v3(0.0f, 0.0f, 0.0f);
+  bool wrote = false;
+  for (int lvl = 1; lvl < maxrec; ++lvl) {              // C/raycast.c:348-376
+    if (!(sc.shapes[obj].refl > 0.0f)) break;
+    D = normalize(reflect(D, N), zero_events);
+    float t;
+    const int i = nearest(sc, O, D, S, t);
+    if (i >= 0) {
+      hit_frame(sc, i, O, D, t, C, N, zero_events);    // writes the carry
+      obj = i;
+      wrote = true;
+    } else {
+      if (MODE == kModeFast) break;                     // CUDA/raycast.cu:224-237
+      if (MODE == kModeParityA && lvl == 1) {
+        po.cls = kClsDep;
+        po.dep = DepRec{D.x, D.y, D.z, N.x, N.y, N.z, obj, 0};
+        return;
+      }
+    }
+    V3 col = shade(sc, i >= 0 ? i : sc.n, C, N, D, zero_events);
+    out.x = out.x + col.x * T;
+    out.y = out.y + col.y * T;
+    out.z = out.z + col.z * T;
+    T = T * sc.shapes[obj].refl;
+    O = C;
+    S = i;
+  }
+  V3 col = shade(sc, i0, P0, N0, d, zero_events);      // C/raycast.c:377-378
+  po.rgb = v3(out.x + col.x, out.y + col.y, out.z + col.z);
+  po.cls = wrote ? kClsWriter : kClsIdent;
+  po.carry = C;
+}
+
+// Carry-only continuation of a DEP pixel from carry-in c (levels 2..maxrec-1): the
+// phase-B transfer function f_p(c).  No shading: only the bounce-hit points matter.
+__device__ __forceinline__ V3 carry_path(const Scene& sc, const DepRec& r, int maxrec, V3 c,
+                                         int& zero_events) {
+  V3 D = v3(r.d1x, r.d1y, r.d1z), N = v3(r.n0x, r.n0y, r.n0z), C = c;
+  int obj = r.obj0, S = -1;
+  for (int lvl = 2; lvl < maxrec; ++lvl) {
+    if (!(sc.shapes[obj].refl > 0.0f)) break;
+    D = normalize(reflect(D, N), zero_events);
+    float t;
+    const int i = nearest(sc, C, D, S, t);
+    if (i >= 0) {
+      V3 P;
+      hit_frame(sc, i, C, D, t, P, N, zero_events);
+      C = P;
+      obj = i;
+    }
+    S = i;
+  }
+  return C;
+}
+
+}  // namespace rc

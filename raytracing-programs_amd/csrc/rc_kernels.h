@@ -1,0 +1,51 @@
+// rc_kernels.h — launch interface between the host runtime (rc_api.hip) and the kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "rc_scene.h"
+
+namespace rc {
+
+// Device view of an uploaded packed scene (rc_scene.h).
+struct LaunchScene {
+  const rc_shape* shapes;
+  const rc_light* lights;
+  const rc_shade_pair* pairs;
+  int n, m;
+  float cam_w, cam_h;
+};
+
+// Parity-mode workspace (device pointers), sized for W*H pixels.
+struct ParityWork {
+  uint8_t* cls;             // [P]   pixel class (ident / writer / dep)
+  float4* wcarry;           // [P]   writer carry-out
+  void* deprec;             // [P]   DepRec (phase A -> B/C)
+  int* row_ndep;            // [H]
+  long long* row_lastw;     // [H]
+  long long* row_lastdep;   // [H]
+  int* row_off;             // [H]
+  long long* row_prevw;     // [H]
+  long long* row_prevdep;   // [H]
+  long long* dep_pix;       // [P]   DEP pixels in scan order
+  long long* dep_key;       // [P]   last writer before each DEP pixel (-1: none)
+  int* seg_start;           // [P]   segment starts (work list, unordered)
+  float4* cin;              // [P]   resolved carry-in per DEP entry
+  int* counters;            // [4]   nseg, dequeue head, ndep, pad
+  int resolve_blocks;       // persistent resolver grid
+  int phase_c_blocks;       // grid-stride phase C grid
+};
+
+hipError_t launch_render(const LaunchScene& s, int W, int H, int row0, int row_step, int nrows,
+                         int maxrec, uint8_t* out, unsigned long long* zcount,
+                         hipStream_t stream);
+
+hipError_t launch_parity(const LaunchScene& s, int W, int H, int maxrec, uint8_t* out,
+                         const ParityWork& w, unsigned long long* zcount, hipStream_t stream,
+                         hipEvent_t ev_a, hipEvent_t ev_b, hipEvent_t ev_c);
+
+size_t deprec_bytes();
+
+}  // namespace rc

@@ -1,0 +1,140 @@
+"""Test helpers: load the package by path and bind the CPU oracle (test infrastructure only)."""
+import ctypes
+import hashlib
+import importlib.util
+import json
+import os
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+SCENES = os.path.join(GOLDEN, "scenes")
+REF_DIR = os.path.join(ROOT, "oracle", "_ref")
+
+
+def load_pkg():
+    name = "raytracing_programs_amd"
+    if name in sys.modules:
+        return sys.modules[name]
+    path = os.path.join(ROOT, "raytracing-programs_amd", "__init__.py")
+    spec = importlib.util.spec_from_file_location(name, path)
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules[name] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
+rc = load_pkg()
+
+
+class RcoStats(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int64) for n in (
+        "sphere_tests", "plane_tests", "quadric_tests", "nearest_calls", "shadow_rays",
+        "bounce_iters", "shaded_hits", "light_evals", "dep_pixels", "dep_writers",
+        "indep_writers", "longest_segment", "zero_normalize", "phantom_shades")] + [
+        ("parity_defined", ctypes.c_int)]
+
+
+_oracle = None
+
+
+def oracle_lib():
+    global _oracle
+    if _oracle is None:
+        lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "build", "liboracle.so"))
+        lib.rco_render.argtypes = [ctypes.POINTER(rc.JsonDataT), ctypes.c_int, ctypes.c_int,
+                                   ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                   ctypes.POINTER(RcoStats), ctypes.c_void_p]
+        lib.rco_load_scene.argtypes = [ctypes.c_char_p, ctypes.POINTER(rc.JsonDataT)]
+        lib.rco_free_scene.argtypes = [ctypes.POINTER(rc.JsonDataT)]
+        _oracle = lib
+    return _oracle
+
+
+def oracle_render(scene, width, height, depth=6, mode="parity", with_carry=False):
+    """CPU restatement (oracle/rc_oracle.c) on the same json_data_t lists."""
+    lib = oracle_lib()
+    img = np.empty((height, width, 3), dtype=np.uint8)
+    st = RcoStats()
+    cin = np.zeros((height, width, 3), dtype=np.float32) if with_carry else None
+    r = lib.rco_render(ctypes.byref(scene.js), width, height, depth + 1, rc.MODES[mode],
+                       img.ctypes.data_as(ctypes.c_void_p), ctypes.byref(st),
+                       cin.ctypes.data_as(ctypes.c_void_p) if with_carry else None)
+    assert r == 0
+    stats = {n: getattr(st, n) for n, _ in RcoStats._fields_}
+    return (img, stats, cin) if with_carry else (img, stats)
+
+
+def golden_table():
+    with open(os.path.join(GOLDEN, "md5.json")) as f:
+        return json.load(f)
+
+
+def golden_key(scene, w, h, depth, mode):
+    return f"{scene}:{w}x{h}:d{depth}:{mode}"
+
+
+def p3_md5(img):
+    """md5 of the reference P3 encoding of img (written by the product P3 writer)."""
+    with tempfile.NamedTemporaryFile(suffix=".ppm", dir="/tmp") as tf:
+        write_p3(img, tf.name)
+        return file_md5(tf.name)
+
+
+class PPMFormat(ctypes.Structure):
+    _fields_ = [("width", ctypes.c_int), ("height", ctypes.c_int), ("size", ctypes.c_int),
+                ("maxColor", ctypes.c_uint8), ("depth", ctypes.c_uint8),
+                ("tupleType", ctypes.c_char_p), ("pixmap", ctypes.c_void_p)]
+
+
+def write_p3(img, path, lib=None):
+    """ppm_WriteOutP3 (product writer by default, or another library exporting it)."""
+    lib = lib or rc.front_lib()
+    lib.ppm_WriteOutP3.argtypes = [PPMFormat, ctypes.c_void_p]
+    h, w, _ = img.shape
+    img = np.ascontiguousarray(img)
+    p = PPMFormat(w, h, w * h * 3, 255, 0, None, img.ctypes.data)
+    libc = ctypes.CDLL(None)
+    libc.fopen.restype = ctypes.c_void_p
+    libc.fopen.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+    libc.fclose.argtypes = [ctypes.c_void_p]
+    f = libc.fopen(os.fsencode(path), b"wb")
+    lib.ppm_WriteOutP3(p, f)
+    libc.fclose(f)
+
+
+def file_md5(path):
+    m = hashlib.md5()
+    with open(path, "rb") as f:
+        for b in iter(lambda: f.read(1 << 24), b""):
+            m.update(b)
+    return m.hexdigest()
+
+
+def have_ref():
+    return os.path.exists(os.path.join(REF_DIR, "raytrace_d6"))
+
+
+def run_ref(scene_path, w, h, depth=6, mode="parity"):
+    """Run the reference build (oracle/_ref) and return the decoded image."""
+    exe = os.path.join(REF_DIR, ("raytrace_fast_d%d" if mode == "fast" else "raytrace_d%d") % depth)
+    with tempfile.TemporaryDirectory(dir="/tmp") as td:
+        out = os.path.join(td, "o.ppm")
+        subprocess.run([exe, str(w), str(h), scene_path, out], check=True,
+                       stdout=subprocess.DEVNULL, cwd=td)
+        return decode_p3(open(out, "rb").read())
+
+
+def decode_p3(data):
+    toks = data.split()
+    assert toks[0] == b"P3"
+    w, h = int(toks[1]), int(toks[2])
+    return np.array([int(t) for t in toks[4:]], dtype=np.uint8).reshape(h, w, 3)
+
+
+def scene_path(name):
+    return os.path.join(SCENES, name + ".scene")

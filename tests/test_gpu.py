@@ -1,0 +1,122 @@
+"""GPU parity tests: libraycast_hip.so (HIP path, called through its C-ABI) against the golden
+md5s of the reference's own output and against the CPU oracle.  Bit-exact: every byte of
+the PPM must match."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from helpers import (GOLDEN, ROOT, file_md5, golden_key, golden_table, oracle_render, p3_md5,
+                     rc, scene_path)
+
+pytestmark = pytest.mark.gpu
+
+SMALL = ["simple", "reflection", "quadric", "example2", "example3", "quadric2"]
+
+
+@pytest.fixture(scope="module")
+def table():
+    return golden_table()
+
+
+@pytest.fixture(scope="module")
+def scenes():
+    return {n: rc.Scene.from_file(scene_path(n)) for n in SMALL}
+
+
+@pytest.mark.parametrize("scene", SMALL)
+@pytest.mark.parametrize("mode", ["parity", "fast"])
+def test_small_goldens(scene, mode, scenes, table):
+    small = np.load(os.path.join(GOLDEN, "small.npz"))
+    for n in (64, 256):
+        for d in (0, 4, 6):
+            img = rc.render(scenes[scene], n, n, depth=d, mode=mode)
+            key = golden_key(scene, n, n, d, mode)
+            if n == 64:
+                np.testing.assert_array_equal(img, small[key], err_msg=key)
+            assert p3_md5(img) == table[key]["md5"], key
+
+
+@pytest.mark.parametrize("key", [
+    "simple:256x256:d6:parity",             # C1
+    "simple:1024x1024:d0:parity",           # C2
+    "reflection:2048x2048:d4:parity",       # C3
+    "reflection:2048x2048:d4:fast",
+    "quadric:4096x4096:d6:parity",          # C4
+    "quadric:4096x4096:d6:fast",
+    "simple:1024x1024:d6:parity", "simple:1024x1024:d6:fast",
+    "reflection:2048x2048:d6:parity", "reflection:2048x2048:d6:fast",
+    "quadric:1024x1024:d6:parity", "quadric:1024x1024:d6:fast",
+    "quadric:512x384:d6:parity", "quadric:333x517:d6:parity", "reflection:1x1:d6:parity",
+    "quadric:7x3:d6:parity", "quadric:1x4096:d6:parity"])
+def test_configs(key, scenes, table):
+    scene, size, d, mode = key.split(":")
+    w, h = map(int, size.split("x"))
+    img = rc.render(scenes[scene], w, h, depth=int(d[1:]), mode=mode)
+    assert p3_md5(img) == table[key]["md5"], key
+
+
+def test_c5_8192(scenes, table):
+    """C5 image (quadric 8192x8192 d6) on one GPU, both modes."""
+    for mode in ("parity", "fast"):
+        img = rc.render(scenes["quadric"], 8192, 8192, depth=6, mode=mode)
+        key = golden_key("quadric", 8192, 8192, 6, mode)
+        assert p3_md5(img) == table[key]["md5"], key
+
+
+def test_oracle_random_sizes(scenes):
+    """GPU == oracle on odd sizes and depths (covers partial tiles and every depth)."""
+    rng = np.random.default_rng(7)
+    for _ in range(6):
+        name = SMALL[int(rng.integers(0, len(SMALL)))]
+        w, h = int(rng.integers(1, 130)), int(rng.integers(1, 130))
+        d = int(rng.integers(0, 8))
+        for mode in ("parity", "fast"):
+            ref, _ = oracle_render(scenes[name], w, h, d, mode)
+            img = rc.render(scenes[name], w, h, depth=d, mode=mode)
+            np.testing.assert_array_equal(img, ref, err_msg=f"{name} {w}x{h} d{d} {mode}")
+
+
+def test_repeat_deterministic(scenes):
+    """The carry resets per call: two renders in one process are identical."""
+    a = rc.render(scenes["quadric"], 300, 200, depth=6)
+    b = rc.render(scenes["quadric"], 300, 200, depth=6)
+    np.testing.assert_array_equal(a, b)
+
+
+def test_cli_dropin(tmp_path, table):
+    """bin/raytrace: same CLI, same P3 bytes, same timing line as C/raycast.c:19-69."""
+    exe = os.path.join(ROOT, "raytracing-programs_amd", "bin", "raytrace")
+    out = tmp_path / "q.ppm"
+    r = subprocess.run([exe, "256", "256", scene_path("quadric"), str(out)],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.startswith("Time (sec) to create a 256x256 image with 5 shape(s) and "
+                               "2 light(s): ")
+    assert file_md5(str(out)) == table["quadric:256x256:d6:parity"]["md5"]
+    env = dict(os.environ, RAYCAST_DEPTH="4", RAYCAST_MODE="fast")
+    r = subprocess.run([exe, "256", "256", scene_path("quadric"), str(out)], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert file_md5(str(out)) == table["quadric:256x256:d4:fast"]["md5"]
+
+
+def test_device_render_matches_host(scenes, table):
+    """rc_render_device (device-resident output, the bench path) writes the same bytes."""
+    torch = pytest.importorskip("torch")
+    out = torch.empty((512, 512, 3), dtype=torch.uint8, device="cuda")
+    rc.render_device(scenes["quadric"], 512, 512, out.data_ptr(),
+                     torch.cuda.current_stream().cuda_stream, depth=6, mode="parity")
+    torch.cuda.synchronize()
+    ref = rc.render(scenes["quadric"], 512, 512, depth=6, mode="parity")
+    np.testing.assert_array_equal(out.cpu().numpy(), ref)
+    # row-cyclic shard (fast mode): rows 1, 4, 7, ... of a 512x512 image
+    rows = (512 - 1 + 2) // 3
+    sh = torch.empty((rows, 512, 3), dtype=torch.uint8, device="cuda")
+    rc.render_device(scenes["quadric"], 512, 512, sh.data_ptr(),
+                     torch.cuda.current_stream().cuda_stream, depth=6, mode="fast", row0=1,
+                     row_step=3, nrows=rows)
+    torch.cuda.synchronize()
+    full = rc.render(scenes["quadric"], 512, 512, depth=6, mode="fast")
+    np.testing.assert_array_equal(sh.cpu().numpy(), full[1::3])

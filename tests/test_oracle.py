@@ -1,0 +1,145 @@
+"""CPU tests: the oracle (oracle/rc_oracle.c) pinned against the reference's own output.
+
+Pinning: tests/golden/md5.json holds the md5 of the P3 images the reference binary itself
+writes (C/ sources built exactly as C/Makefile:4, tests/golden/make_golden.py), and
+small.npz the decoded 64x64 images.  When oracle/_ref is present the oracle is also
+compared image-for-image with the reference on seeded random scenes.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from helpers import (GOLDEN, SCENES, golden_key, golden_table, have_ref, oracle_render, p3_md5,
+                     rc, run_ref, scene_path)
+
+SMALL = ["simple", "reflection", "quadric", "example2", "example3", "quadric2"]
+
+
+@pytest.fixture(scope="module")
+def table():
+    return golden_table()
+
+
+@pytest.mark.parametrize("scene", SMALL)
+@pytest.mark.parametrize("mode", ["parity", "fast"])
+def test_oracle_small_goldens(scene, mode, table):
+    """Every 64x64 and 256x256 golden (depth 0/4/6) — SURVEY.md Appendix B/B2."""
+    s = rc.Scene.from_file(scene_path(scene))
+    small = np.load(os.path.join(GOLDEN, "small.npz"))
+    for n in (64, 256):
+        for d in (0, 4, 6):
+            img, _ = oracle_render(s, n, n, d, mode)
+            key = golden_key(scene, n, n, d, mode)
+            assert p3_md5(img) == table[key]["md5"], key
+            if n == 64:
+                np.testing.assert_array_equal(img, small[key])
+
+
+@pytest.mark.parametrize("key", ["simple:1024x1024:d0:parity", "reflection:2048x2048:d4:parity",
+                                 "reflection:2048x2048:d4:fast", "quadric:512x384:d6:parity",
+                                 "quadric:333x517:d6:parity", "reflection:1x1:d6:parity",
+                                 "quadric:7x3:d6:parity", "quadric:1x4096:d6:parity"])
+def test_oracle_configs(key, table):
+    """BASELINE configs C2/C3 plus ragged and degenerate image shapes."""
+    scene, size, d, mode = key.split(":")
+    w, h = map(int, size.split("x"))
+    s = rc.Scene.from_file(scene_path(scene))
+    img, _ = oracle_render(s, w, h, int(d[1:]), mode)
+    assert p3_md5(img) == table[key]["md5"]
+
+
+@pytest.mark.skipif(not os.environ.get("RC_SLOW"), reason="12 s: set RC_SLOW=1")
+def test_oracle_c4(table):
+    s = rc.Scene.from_file(scene_path("quadric"))
+    img, st = oracle_render(s, 4096, 4096, 6, "parity")
+    assert p3_md5(img) == table["quadric:4096x4096:d6:parity"]["md5"]
+    assert st["dep_pixels"] == 2804464 and st["longest_segment"] == 844249
+
+
+def test_oracle_stats_match_survey():
+    """Work counts at C1 — these feed the roofline's flop/pixel."""
+    s = rc.Scene.from_file(scene_path("simple"))
+    _, st = oracle_render(s, 256, 256, 6, "parity")
+    n = 256 * 256
+    assert abs(st["sphere_tests"] / n - 7.631) < 1e-3
+    assert abs(st["plane_tests"] / n - 2.146) < 1e-3
+    assert st["dep_pixels"] == 7868
+    assert st["parity_defined"] == 1
+
+
+def _random_scene(rng, path, n_shapes, n_lights):
+    """A phantom-safe random scene in the reference grammar (lights keep the phantom black:
+    1 light with color[0]+color[1] >= 1; 2 lights with L1.pos.y + L1.pos.z >= 1)."""
+    lines = ["camera, width: 2.0, height: 2.0"]
+    for _ in range(n_shapes):
+        kind = rng.choice(["sphere", "sphere", "plane", "quadric"])
+        dif = ", ".join(f"{v:.3f}" for v in rng.uniform(0, 1, 3))
+        spe = ", ".join(f"{v:.3f}" for v in rng.uniform(0, 1, 3))
+        refl = rng.uniform(0, 0.8)
+        if kind == "sphere":
+            pos = [rng.uniform(-4, 4), rng.uniform(-3, 3), rng.uniform(-15, -4)]
+            lines.append(f"sphere, radius: {rng.uniform(0.3, 2.0):.3f}, diffuse_color: [{dif}], "
+                         f"specular_color: [{spe}], position: [{pos[0]:.3f}, {pos[1]:.3f}, "
+                         f"{pos[2]:.3f}], reflectivity: {refl:.3f}, refractivity: "
+                         f"{rng.uniform(0, 0.2):.3f}, ior: 1.33")
+        elif kind == "plane":
+            nrm = rng.normal(size=3)
+            nrm[1] = abs(nrm[1]) + 1
+            lines.append(f"plane, normal: [{nrm[0]:.3f}, {nrm[1]:.3f}, {nrm[2]:.3f}], "
+                         f"diffuse_color: [{dif}], position: [0, {rng.uniform(-5, -1):.3f}, 0], "
+                         f"reflectivity: {refl:.3f}")
+        else:
+            a, b, c = rng.uniform(-1, 4, 3)
+            g, h, i = rng.uniform(-20, 20, 3)
+            lines.append(f"quadric, diffuse_color: [{dif}], specular_color: [{spe}], a: {a:.2f}, "
+                         f"b: {b:.2f}, c: {c:.2f}, d: 0, e: 0, f: 0, g: {g:.2f}, h: {h:.2f}, "
+                         f"i: {i:.2f}, j: {rng.uniform(50, 300):.2f}, reflectivity: {refl:.3f}")
+    for k in range(n_lights):
+        col = rng.uniform(0.6, 4, 3)
+        pos = [rng.uniform(-10, 10), rng.uniform(1, 10), rng.uniform(-10, 2)]
+        spot = n_lights == 2 and k == 0 and rng.uniform() < 0.5
+        extra = (f", theta: {rng.uniform(1, 20):.2f}, angular-a0: {int(rng.integers(0, 4))}, "
+                 f"direction: [0, 0, -1]") if spot else ""
+        lines.append(f"light, color: [{col[0]:.2f}, {col[1]:.2f}, {col[2]:.2f}], radial-a2: 0.01, "
+                     f"radial-a1: 0.0125, radial-a0: 0.0125, position: [{pos[0]:.2f}, "
+                     f"{pos[1]:.2f}, {pos[2]:.2f}]{extra}")
+    with open(path, "w") as f:
+        f.write("\n".join(lines) + "\n")
+
+
+@pytest.mark.skipif(not have_ref(), reason="oracle/_ref not built (make ref)")
+@pytest.mark.parametrize("seed", range(8))
+def test_oracle_vs_reference_random_scenes(seed, tmp_path):
+    rng = np.random.default_rng(seed)
+    path = str(tmp_path / f"r{seed}.scene")
+    _random_scene(rng, path, int(rng.integers(2, 9)), int(rng.integers(1, 3)))
+    s = rc.Scene.from_file(path)
+    for mode in ("parity", "fast"):
+        for d in (1, 6):
+            img, st = oracle_render(s, 48, 40, d, mode)
+            if not st["parity_defined"]:
+                continue
+            np.testing.assert_array_equal(img, run_ref(path, 48, 40, d, mode))
+
+
+@pytest.mark.skipif(not have_ref(), reason="oracle/_ref not built (make ref)")
+def test_phantom_model_four_lights(tmp_path):
+    """shapes_list[-1] with 4 lights = light-VLA bytes [184, 288): diffuse/specular from
+    L2 (cos_theta, a0, direction, type) and reflectivity/refractivity = L3.pos[1], pos[2].
+    Chosen so the phantom is lit (opacity > 0): the image depends on the model."""
+    path = str(tmp_path / "ph4.scene")
+    with open(path, "w") as f:
+        f.write(open(scene_path("quadric")).read().rstrip("\n").replace(
+            "light, color: [4, 4, 4], radial-a2: 0.01, radial-a1: 0.0125, radial-a0: 0.0125, "
+            "position: [10, 10, -5]",
+            "light, color: [4, 4, 4], radial-a2: 0.01, radial-a1: 0.0125, radial-a0: 0.0125, "
+            "position: [10, 10, -5]\n"
+            "light, color: [1, 1, 1], radial-a2: 0.05, radial-a1: 0.1, radial-a0: 0.1, "
+            "position: [-3, 4, 2], theta: 0.3, angular-a0: 1, direction: [0.3, 0.2, 0.9]\n"
+            "light, color: [0.5, 0.5, 0.5], radial-a2: 0.05, radial-a1: 0.1, radial-a0: 0.1, "
+            "position: [2, 0.25, 0.125]") + "\n")
+    s = rc.Scene.from_file(path)
+    img, st = oracle_render(s, 96, 96, 6, "parity")
+    assert st["parity_defined"] == 1 and st["phantom_shades"] > 0
+    np.testing.assert_array_equal(img, run_ref(path, 96, 96, 6, "parity"))
