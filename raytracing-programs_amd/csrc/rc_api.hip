@@ -66,7 +66,10 @@ struct DevCtx {
   DevBuf scene;        // uploaded packed scene
   const void* scene_src = nullptr;   // host image last uploaded
   // parity workspace
-  DevBuf cls, wcarry, deprec, rows, dep_pix, dep_key, seg_start, cin, counters;
+  DevBuf cls, wcarry, deprec, rows, dep_pix, dep_key, dep_rec, seg_flag, blk_cnt, seg_start,
+      cin, counters, team, trace;
+  int resident_blocks = 0;
+  int resident_lds = -1;
   size_t parity_pixels = 0;
   int parity_rows = 0;
 };
@@ -176,9 +179,18 @@ int ensure_parity(DevCtx& c, int W, int H, rc::ParityWork& w) {
       c.deprec.ensure(P * rc::deprec_bytes()) ||
       c.rows.ensure((size_t)H * (2 * sizeof(int) + 4 * sizeof(long long)) + 256) ||
       c.dep_pix.ensure(P * sizeof(long long)) || c.dep_key.ensure(P * sizeof(long long)) ||
+      c.dep_rec.ensure(P * rc::deprec_bytes()) || c.seg_flag.ensure(P) ||
+      c.blk_cnt.ensure((P / 1024 + 2) * sizeof(int)) ||
       c.seg_start.ensure(P * sizeof(int)) || c.cin.ensure(P * sizeof(float4)) ||
-      c.counters.ensure(64))
+      c.counters.ensure(64) || c.team.ensure(rc::team_state_bytes()))
     return -1;
+  if (P >= (size_t)1 << 31) return -1;   // DEP indices are 32-bit
+  const int one_per_cu = std::getenv("RC_RESOLVE_SHARED") ? 0 : 1;
+  const int lds = one_per_cu ? 96 * 1024 : 0;
+  if (!c.resident_blocks || c.resident_lds != lds) {
+    c.resident_blocks = rc::resolve_blocks_resident(c.cus, lds);
+    c.resident_lds = lds;
+  }
   char* r = (char*)c.rows.p;
   w.cls = (uint8_t*)c.cls.p;
   w.wcarry = (float4*)c.wcarry.p;
@@ -191,10 +203,34 @@ int ensure_parity(DevCtx& c, int W, int H, rc::ParityWork& w) {
   w.row_off = (int*)r;
   w.dep_pix = (long long*)c.dep_pix.p;
   w.dep_key = (long long*)c.dep_key.p;
+  w.dep_rec = c.dep_rec.p;
+  w.seg_flag = (uint8_t*)c.seg_flag.p;
+  w.blk_cnt = (int*)c.blk_cnt.p;
   w.seg_start = (int*)c.seg_start.p;
   w.cin = (float4*)c.cin.p;
   w.counters = (int*)c.counters.p;
-  w.resolve_blocks = c.cus * 4;
+  w.team = c.team.p;
+  // The team spins on a counter barrier: its blocks (the first of the grid) and the grid as
+  // a whole must be co-resident, so the grid never exceeds the resident capacity.
+  w.resolve_blocks = c.resident_blocks;
+  w.resolve_lds = c.resident_lds;
+  w.team_blocks = std::getenv("RC_TEAM_BLOCKS") ? std::atoi(std::getenv("RC_TEAM_BLOCKS")) : 128;
+  if (w.team_blocks > 256) w.team_blocks = 256;
+  if (w.team_blocks > w.resolve_blocks / 2) w.team_blocks = w.resolve_blocks / 2;
+  w.long_len = std::getenv("RC_LONG_LEN") ? std::atoi(std::getenv("RC_LONG_LEN")) : 32768;
+  w.team_coop = std::getenv("RC_TEAM_MODE") ? std::atoi(std::getenv("RC_TEAM_MODE")) : 1;
+  w.coop_group = 0;
+  if (!std::getenv("RC_NO_COOP") && c.scene_src) {
+    const int n = ((const rc_packed_header*)c.scene_src)->n;
+    int g = 1;
+    while (g < n) g <<= 1;
+    if (n >= 1 && g <= 64) w.coop_group = g;
+  }
+  w.trace = nullptr;
+  if (std::getenv("RC_RESOLVE_TRACE")) {
+    if (c.trace.ensure(P * 2 * sizeof(unsigned))) return -1;
+    w.trace = (unsigned*)c.trace.p;
+  }
   w.phase_c_blocks = c.cus * 8;
   return 0;
 }
@@ -248,6 +284,23 @@ void fill_device_timing(DevCtx& c, const rc_options* opt, rc_timing* t) {
     int cnt[4] = {0, 0, 0, 0};
     if (hipMemcpy(cnt, c.counters.p, sizeof cnt, hipMemcpyDeviceToHost) == hipSuccess)
       t->dep_pixels = cnt[2];
+    const char* path = std::getenv("RC_RESOLVE_TRACE");
+    if (path && c.trace.p && cnt[0] > 0) {   // debug: per-segment resolver trace
+      std::vector<int> starts(cnt[0]);
+      std::vector<unsigned> tr(2 * (size_t)cnt[0]);
+      (void)hipMemcpy(starts.data(), c.seg_start.p, starts.size() * sizeof(int),
+                      hipMemcpyDeviceToHost);
+      (void)hipMemcpy(tr.data(), c.trace.p, tr.size() * sizeof(unsigned), hipMemcpyDeviceToHost);
+      if (FILE* f = std::fopen(path, "w")) {
+        std::fprintf(f, "# seg start len ticks_100MHz evals(team: rounds|0x80000000)\n");
+        for (int k = 0; k < cnt[0]; ++k) {
+          const int end = k + 1 < cnt[0] ? starts[k + 1] : cnt[2];
+          std::fprintf(f, "%d %d %d %u %u\n", k, starts[k], end - starts[k], tr[2 * k],
+                       tr[2 * k + 1]);
+        }
+        std::fclose(f);
+      }
+    }
   }
 }
 

@@ -456,3 +456,133 @@ __device__ __forceinline__ V3 carry_path(const Scene& sc, const DepRec& r, int m
 }
 
 }  // namespace rc
+
+namespace rc {
+
+// ---------------------------------------------------------- cooperative evaluation --
+// One entry's transfer function evaluated by a group of G lanes (G = power of two >= n):
+// lane k of the group tests shape k, then the group takes the lexicographic minimum of
+// (t, k) over the valid candidates.  That is exactly the reference's nearest object
+// (C/raycast.c:449-528): the scan accepts strictly smaller t in file order, so the winner
+// is the smallest valid t and, among equal t, the smallest index.  The latency of a level is
+// one shape test (per type present) instead of n of them.
+struct LaneShape {
+  rc_shape s;
+  bool has;
+};
+
+__device__ __forceinline__ int group_argmin(float& t, int k, int G) {
+  for (int off = 1; off < G; off <<= 1) {
+    const float t2 = __shfl_xor(t, off, 64);
+    const int k2 = __shfl_xor(k, off, 64);
+    if (t2 < t || (t2 == t && k2 < k)) {
+      t = t2;
+      k = k2;
+    }
+  }
+  return k;
+}
+
+__device__ __forceinline__ V3 carry_path_coop(const Scene& sc, const LaneShape& ls, int kself,
+                                              int G, const DepRec& r, int maxrec, V3 c,
+                                              int& zero_events) {
+  constexpr int kNone = 0x7fffffff;
+  V3 D = v3(r.d1x, r.d1y, r.d1z), N = v3(r.n0x, r.n0y, r.n0z), C = c;
+  int obj = r.obj0, S = -1;
+  for (int lvl = 2; lvl < maxrec; ++lvl) {
+    if (!(sc.shapes[obj].refl > 0.0f)) break;
+    D = normalize(reflect(D, N), zero_events);
+    const RayK rk = ray_consts(D);
+    float t = __builtin_inff();
+    int k = kNone;
+    if (ls.has && kself != S) {
+      float tt = 0.0f;
+      if (test_shape(ls.s, C, D, rk, S, tt) && __builtin_inff() > tt && tt > 0.0f) {
+        t = tt;
+        k = kself;
+      }
+    }
+    const int win = group_argmin(t, k, G);
+    if (win != kNone) {
+      V3 P;
+      hit_frame(sc, win, C, D, t, P, N, zero_events);
+      C = P;
+      obj = win;
+      S = win;
+    } else {
+      S = -1;
+    }
+  }
+  return C;
+}
+
+}  // namespace rc
+
+namespace rc {
+
+// Cooperative evaluation with level speculation: the 2G lanes of one entry form two
+// groups.  Group h=0 evaluates bounce level L; group h=1 evaluates level L+1 assuming level
+// L misses — then its ray is fully known in advance: same origin C, direction
+// normalize(reflect(D_L, N)), skip -1, and the object test refl[obj] > 0 unchanged
+// (C/raycast.c:349-367 with the stale object/normal of a miss).  If level L misses, both
+// levels retire in one step.  The carry creep of dense segments alternates hit/miss, so
+// five levels retire in three steps.
+__device__ __forceinline__ V3 carry_path_spec(const Scene& sc, const LaneShape& ls, int kself,
+                                              int G, int half, const DepRec& r, int maxrec,
+                                              V3 c, int& zero_events) {
+  constexpr int kNone = 0x7fffffff;
+  V3 D = v3(r.d1x, r.d1y, r.d1z), N = v3(r.n0x, r.n0y, r.n0z), C = c;
+  int obj = r.obj0, S = -1;
+  const int lane = threadIdx.x & 63;
+  const int lead0 = lane & ~(2 * G - 1);   // group h=0 leader of this entry
+  const int lead1 = lead0 + G;             // group h=1 leader
+  int lvl = 2;
+  while (lvl < maxrec) {
+    if (!(sc.shapes[obj].refl > 0.0f)) break;
+    const V3 D1 = normalize(reflect(D, N), zero_events);
+    const V3 D2 = normalize(reflect(D1, N), zero_events);
+    const V3 myD = half ? D2 : D1;
+    const int myS = half ? -1 : S;
+    const RayK rk = ray_consts(myD);
+    float t = __builtin_inff();
+    int k = kNone;
+    if (ls.has && kself != myS) {
+      float tt = 0.0f;
+      if (test_shape(ls.s, C, myD, rk, myS, tt) && __builtin_inff() > tt && tt > 0.0f) {
+        t = tt;
+        k = kself;
+      }
+    }
+    k = group_argmin(t, k, G);
+    const int w0 = __shfl(k, lead0, 64), w1 = __shfl(k, lead1, 64);
+    const float t0 = __shfl(t, lead0, 64), t1 = __shfl(t, lead1, 64);
+    if (w0 != kNone) {                       // level L hits
+      V3 P;
+      hit_frame(sc, w0, C, D1, t0, P, N, zero_events);
+      C = P;
+      obj = w0;
+      S = w0;
+      D = D1;
+      lvl += 1;
+    } else if (lvl + 1 < maxrec) {           // level L misses: level L+1 was speculated
+      if (w1 != kNone) {
+        V3 P;
+        hit_frame(sc, w1, C, D2, t1, P, N, zero_events);
+        C = P;
+        obj = w1;
+        S = w1;
+      } else {
+        S = -1;
+      }
+      D = D2;
+      lvl += 2;
+    } else {
+      S = -1;
+      D = D1;
+      lvl += 1;
+    }
+  }
+  return C;
+}
+
+}  // namespace rc

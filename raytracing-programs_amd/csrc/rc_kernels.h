@@ -31,11 +31,21 @@ struct ParityWork {
   long long* row_prevdep;   // [H]
   long long* dep_pix;       // [P]   DEP pixels in scan order
   long long* dep_key;       // [P]   last writer before each DEP pixel (-1: none)
-  int* seg_start;           // [P]   segment starts (work list, unordered)
+  void* dep_rec;            // [P]   DepRec of each DEP entry, scan order
+  uint8_t* seg_flag;        // [P]   1 where a segment starts
+  int* blk_cnt;             // [P/1024] flag counts -> offsets
+  int* seg_start;           // [P]   segment starts, in scan order
   float4* cin;              // [P]   resolved carry-in per DEP entry
   int* counters;            // [4]   nseg, dequeue head, ndep, pad
-  int resolve_blocks;       // persistent resolver grid
+  void* team;               // TeamState of the long-segment team
+  int resolve_blocks;       // persistent resolver grid (<= resident capacity)
+  int resolve_lds;          // dynamic LDS per resolver block (occupancy control)
+  int team_blocks;          // workgroups in the long-segment team (0: no team)
+  int long_len;             // segments with >= long_len entries go to the team
   int phase_c_blocks;       // grid-stride phase C grid
+  int team_coop;            // team rounds use the cooperative evaluator
+  int coop_group;           // lanes per entry of the cooperative evaluator (0: off)
+  unsigned* trace;          // optional [2*nseg] per-segment {ticks, evals} (debug)
 };
 
 hipError_t launch_render(const LaunchScene& s, int W, int H, int row0, int row_step, int nrows,
@@ -47,5 +57,7 @@ hipError_t launch_parity(const LaunchScene& s, int W, int H, int maxrec, uint8_t
                          hipEvent_t ev_a, hipEvent_t ev_b, hipEvent_t ev_c);
 
 size_t deprec_bytes();
+size_t team_state_bytes();
+int resolve_blocks_resident(int cus, int lds_bytes);
 
 }  // namespace rc

@@ -202,13 +202,14 @@ __global__ void __launch_bounds__(1024) k_row_scan(int H, const int* __restrict_
   if (threadIdx.x == 0) *ndep_total = carry_cnt;
 }
 
-// Per row: write the DEP pixels in scan order with their segment key (last writer before
-// the pixel, -1 = none: carry (0,0,0)) and append segment starts to the work list.
+// Per row: write the DEP pixels in scan order (compact DepRec + pixel id), their segment key
+// (last writer before the pixel, -1 = none: carry (0,0,0)) and a segment-start flag.
 __global__ void __launch_bounds__(kScanBlock) k_row_compact(
     const uint8_t* __restrict__ cls, int W, const int* __restrict__ row_off,
     const long long* __restrict__ row_prevw, const long long* __restrict__ row_prevdep,
+    const DepRec* __restrict__ deprec, DepRec* __restrict__ dep_rec,
     long long* __restrict__ dep_pix, long long* __restrict__ dep_key,
-    int* __restrict__ seg_start, int* __restrict__ nseg) {
+    uint8_t* __restrict__ seg_flag) {
   __shared__ int s_cnt[kScanBlock];
   __shared__ long long s_w[kScanBlock], s_d[kScanBlock];
   __shared__ int c_cnt;
@@ -253,7 +254,8 @@ __global__ void __launch_bounds__(kScanBlock) k_row_compact(
       if (c_d > prevd) prevd = c_d;
       dep_pix[idx] = pix;
       dep_key[idx] = key;
-      if (prevd < 0 || key > prevd) seg_start[atomicAdd(nseg, 1)] = idx;
+      dep_rec[idx] = deprec[pix];
+      seg_flag[idx] = (prevd < 0 || key > prevd) ? 1 : 0;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -265,8 +267,81 @@ __global__ void __launch_bounds__(kScanBlock) k_row_compact(
   }
 }
 
+// Ordered segment table: flag count per 1024 entries -> one-block scan -> scatter.
+constexpr int kFlagBlock = 1024;
+
+__global__ void __launch_bounds__(kFlagBlock) k_flag_count(const uint8_t* __restrict__ flag,
+                                                           const int* __restrict__ ndep_p,
+                                                           int* __restrict__ blk_cnt) {
+  __shared__ int sh[16];
+  const int ndep = *ndep_p;
+  const long long i = (long long)blockIdx.x * kFlagBlock + threadIdx.x;
+  if ((long long)blockIdx.x * kFlagBlock >= ndep) return;
+  int v = (i < ndep) ? flag[i] : 0;
+  v = block_sum(v, sh);
+  if (threadIdx.x == 0) blk_cnt[blockIdx.x] = v;
+}
+
+__global__ void __launch_bounds__(1024) k_flag_scan(const int* __restrict__ ndep_p,
+                                                    int* __restrict__ blk_cnt,
+                                                    int* __restrict__ nseg_p) {
+  __shared__ int s[1024];
+  __shared__ int carry;
+  const int nblk = (*ndep_p + kFlagBlock - 1) / kFlagBlock;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (int b0 = 0; b0 < nblk; b0 += 1024) {
+    const int b = b0 + threadIdx.x;
+    const int v = b < nblk ? blk_cnt[b] : 0;
+    s[threadIdx.x] = v;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {
+      const int u = (int)threadIdx.x >= o ? s[threadIdx.x - o] : 0;
+      __syncthreads();
+      s[threadIdx.x] += u;
+      __syncthreads();
+    }
+    if (b < nblk) blk_cnt[b] = carry + s[threadIdx.x] - v;   // exclusive offset
+    __syncthreads();
+    if (threadIdx.x == 0) carry += s[1023];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *nseg_p = carry;
+}
+
+__global__ void __launch_bounds__(kFlagBlock) k_flag_scatter(const uint8_t* __restrict__ flag,
+                                                             const int* __restrict__ ndep_p,
+                                                             const int* __restrict__ blk_off,
+                                                             int* __restrict__ seg_start) {
+  __shared__ int s[kFlagBlock];
+  const int ndep = *ndep_p;
+  if ((long long)blockIdx.x * kFlagBlock >= ndep) return;
+  const long long i = (long long)blockIdx.x * kFlagBlock + threadIdx.x;
+  const int v = (i < ndep) ? flag[i] : 0;
+  s[threadIdx.x] = v;
+  __syncthreads();
+  for (int o = 1; o < kFlagBlock; o <<= 1) {
+    const int u = (int)threadIdx.x >= o ? s[threadIdx.x - o] : 0;
+    __syncthreads();
+    s[threadIdx.x] += u;
+    __syncthreads();
+  }
+  if (v) seg_start[blk_off[blockIdx.x] + s[threadIdx.x] - 1] = (int)i;
+}
+
 // ------------------------------------------------------------ parity phase B: carry --
+// The carry chain of one segment (DEP entries [start, end), initial carry from the writer
+// before it) is resolved exactly: evaluate the transfer function f_p (carry_path) of a window
+// of entries at the current carry in parallel; the FIRST entry whose output differs bitwise
+// from its input is the next place the carry changes.  A wave keeps its 64 records in
+// registers and re-evaluates only the lanes after each changer (ballot + shuffle, no barrier),
+// so a changer costs one f_p latency.  Segments longer than `long_len` entries (one or two per
+// image, up to ~10^6 entries) are resolved by a TEAM of workgroups that evaluate a
+// team_blocks*256-entry window per round and agree on the first changer through a counter
+// barrier (all team blocks are co-resident: they are the first blocks of a grid sized to the
+// device's resident capacity).
 constexpr int kResolveBlock = 256;
+constexpr int kTeamMax = 256;
 
 __device__ __forceinline__ bool same_bits(V3 a, V3 b) {
   return __float_as_uint(a.x) == __float_as_uint(b.x) &&
@@ -274,70 +349,285 @@ __device__ __forceinline__ bool same_bits(V3 a, V3 b) {
          __float_as_uint(a.z) == __float_as_uint(b.z);
 }
 
-__global__ void __launch_bounds__(kResolveBlock) k_resolve(
-    Scene sc, int maxrec, const long long* __restrict__ dep_pix,
-    const long long* __restrict__ dep_key, const DepRec* __restrict__ deprec,
-    const float4* __restrict__ wcarry, const int* __restrict__ seg_start,
-    const int* __restrict__ nseg_p, const int* __restrict__ ndep_p, int* __restrict__ head,
-    float4* __restrict__ cin) {
-  __shared__ int s_seg, s_first, s_nvalid;
-  __shared__ float s_c[3];
-  const int nseg = *nseg_p;
-  const int ndep = *ndep_p;
-  for (;;) {
-    if (threadIdx.x == 0) s_seg = atomicAdd(head, 1);
-    __syncthreads();
-    const int seg = s_seg;
-    __syncthreads();
-    if (seg >= nseg) break;
-    int j = seg_start[seg];
-    const long long key = dep_key[j];
-    V3 carry = v3(0.0f, 0.0f, 0.0f);
-    if (key >= 0) {
-      const float4 k4 = wcarry[key];
-      carry = v3(k4.x, k4.y, k4.z);
+__device__ __forceinline__ V3 seg_init_carry(const long long* __restrict__ dep_key,
+                                             const float4* __restrict__ wcarry, int start) {
+  const long long key = dep_key[start];
+  if (key < 0) return v3(0.0f, 0.0f, 0.0f);
+  const float4 k4 = wcarry[key];
+  return v3(k4.x, k4.y, k4.z);
+}
+
+// Resolve the 64 entries [base, base+64) ∩ [.., end) of one wave at carry `c`, changers
+// included.  On return: `mine` = this lane's carry-in, `c` = carry after the window; the
+// result counts transfer-function evaluation steps.  The first pass evaluates the 64
+// entries one per lane.  After a changer the rest of the window is dense-prone (the carry
+// creeps one entry at a time in long runs), so it continues with the cooperative evaluator:
+// 64/G entries per step, shapes spread over the G lanes of each group.
+__device__ __forceinline__ DepRec shfl_rec(const DepRec& r, int src) {
+  DepRec o;
+  o.d1x = __shfl(r.d1x, src, 64);
+  o.d1y = __shfl(r.d1y, src, 64);
+  o.d1z = __shfl(r.d1z, src, 64);
+  o.n0x = __shfl(r.n0x, src, 64);
+  o.n0y = __shfl(r.n0y, src, 64);
+  o.n0z = __shfl(r.n0z, src, 64);
+  o.obj0 = __shfl(r.obj0, src, 64);
+  o.pad = 0;
+  return o;
+}
+
+__device__ __forceinline__ int wave_window(const Scene& sc, int maxrec,
+                                           const DepRec* __restrict__ dep_rec, int base,
+                                           int end, V3& c, V3& mine, const LaneShape& ls,
+                                           int G) {
+  const int lane = threadIdx.x & 63;
+  const int idx = base + lane;
+  const int nvalid = end - base < 64 ? end - base : 64;
+  const bool valid = lane < nvalid;
+  DepRec r;
+  if (valid) r = dep_rec[idx];
+  mine = c;
+  int zero = 0;
+  V3 o = c;
+  if (valid) o = carry_path(sc, r, maxrec, c, zero);
+  unsigned long long m = __ballot(valid && !same_bits(o, c));
+  int evals = 1;
+  if (m == 0) return evals;
+  int k = __ffsll((long long)m) - 1;
+  c = v3(__shfl(o.x, k, 64), __shfl(o.y, k, 64), __shfl(o.z, k, 64));
+  int pos = k + 1;   // lanes < pos resolved (their mine is the carry they were read with)
+  if (G > 0) {
+    // speculative pairs when two groups fit per entry, else one group per entry
+    const bool spec = 2 * G <= 64;
+    const int GE = spec ? 2 * G : G;          // lanes per entry
+    const int E = 64 / GE;
+    const int e = lane / GE, kself = lane % G, half = spec ? (lane / G) & 1 : 0;
+    while (pos < nvalid) {
+      ++evals;
+      const int i = pos + e;
+      const bool act = e < E && i < nvalid;
+      const DepRec ri = shfl_rec(r, i < 64 ? i : 63);
+      V3 oc = c;
+      if (act)
+        oc = spec ? carry_path_spec(sc, ls, kself, G, half, ri, maxrec, c, zero)
+                  : carry_path_coop(sc, ls, kself, G, ri, maxrec, c, zero);
+      const unsigned long long mc = __ballot(act && (lane % GE) == 0 && !same_bits(oc, c));
+      if (mc == 0) {
+        const int lim = pos + E < nvalid ? pos + E : nvalid;
+        if (lane >= pos && lane < lim) mine = c;
+        pos = lim;
+        continue;
+      }
+      const int g = (__ffsll((long long)mc) - 1) / GE;
+      if (lane >= pos && lane <= pos + g) mine = c;
+      c = v3(__shfl(oc.x, g * GE, 64), __shfl(oc.y, g * GE, 64), __shfl(oc.z, g * GE, 64));
+      pos += g + 1;
     }
-    for (;;) {
-      if (threadIdx.x == 0) {
-        s_first = kResolveBlock;
-        s_nvalid = kResolveBlock;
-      }
-      __syncthreads();
-      const int jj = j + (int)threadIdx.x;
-      const bool valid = jj < ndep && dep_key[jj] == key;
-      V3 o = carry;
-      bool changed = false;
-      if (valid) {
-        int zero = 0;
-        o = carry_path(sc, deprec[dep_pix[jj]], maxrec, carry, zero);
-        changed = !same_bits(o, carry);
-      } else {
-        atomicMin(&s_nvalid, (int)threadIdx.x);
-      }
-      if (changed) atomicMin(&s_first, (int)threadIdx.x);
-      __syncthreads();
-      const int first = s_first, nvalid = s_nvalid;
-      const int lim = first < kResolveBlock ? first + 1 : nvalid;
-      if ((int)threadIdx.x < lim) cin[jj] = make_float4(carry.x, carry.y, carry.z, 0.0f);
-      if ((int)threadIdx.x == first) {
-        s_c[0] = o.x;
-        s_c[1] = o.y;
-        s_c[2] = o.z;
-      }
-      __syncthreads();
-      if (first < kResolveBlock) {
-        carry = v3(s_c[0], s_c[1], s_c[2]);
-        j += first + 1;
-        __syncthreads();
-        continue;
-      }
-      if (nvalid == kResolveBlock) {
-        j += kResolveBlock;
-        continue;
-      }
+    return evals;
+  }
+  // no cooperative evaluator (more than 64 shapes): per-lane steps
+  bool active = valid && lane >= pos;
+  while (__ballot(active)) {
+    ++evals;
+    if (active) o = carry_path(sc, r, maxrec, c, zero);
+    m = __ballot(active && !same_bits(o, c));
+    if (m == 0) {
+      if (active) mine = c;
       break;
     }
-    __syncthreads();
+    k = __ffsll((long long)m) - 1;
+    if (active && lane <= k) mine = c;
+    c = v3(__shfl(o.x, k, 64), __shfl(o.y, k, 64), __shfl(o.z, k, 64));
+    active = active && lane > k;
+  }
+  return evals;
+}
+
+// 8-byte granules: {first changed wave (-1: none), carry.x}, {carry.y, carry.z}
+struct alignas(16) TeamSlot {
+  unsigned long long g0, g1;
+};
+__device__ __forceinline__ unsigned long long pack2(unsigned lo, unsigned hi) {
+  return (unsigned long long)lo | ((unsigned long long)hi << 32);
+}
+
+struct TeamState {
+  int arrive;       // monotonic arrival counter (one add per block per round)
+  int error;        // spin timeout
+  int pad[30];
+  TeamSlot slot[2][kTeamMax];
+};
+
+// Counter barrier over the team's blocks.  The hand-off follows MI355X_MICROARCH.md's
+// fence-free row: each block's slot is written by ONE lane with agent-scope (sc1) stores, that
+// lane drains them (s_waitcnt vmcnt(0)) before its agent-scope counter add, and consumers
+// poll the counter and read slots with sc1 loads only.  The spin is bounded (5 s) and
+// reports a timeout through ts->error instead of hanging.
+__device__ __forceinline__ void team_barrier(TeamState* ts, int target) {
+  if (threadIdx.x == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_fetch_add(&ts->arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(&ts->arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      if (__builtin_amdgcn_s_memrealtime() - t0 > 500000000ull) {   // 5 s at 100 MHz
+        __hip_atomic_store(&ts->error, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+}
+
+__global__ void __launch_bounds__(kResolveBlock) k_resolve(
+    Scene sc, int maxrec, const DepRec* __restrict__ dep_rec,
+    const long long* __restrict__ dep_key, const float4* __restrict__ wcarry,
+    const int* __restrict__ seg_start, const int* __restrict__ counters, int* __restrict__ head,
+    float4* __restrict__ cin, int team_blocks, int long_len, TeamState* __restrict__ ts,
+    unsigned* __restrict__ trace, int G, int team_coop) {
+  const int nseg = counters[0];
+  const int ndep = counters[2];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  LaneShape ls;
+  ls.has = false;
+  if (G > 0) {
+    const int kself = lane % G;
+    ls.has = kself < sc.n;
+    if (ls.has) ls.s = sc.shapes[kself];
+  }
+
+  if ((int)blockIdx.x < team_blocks) {
+    // ------------------------------------------------------------------- team --
+    // One round = every member wave evaluates its 64 entries once at the current carry and
+    // reports its first changer; the team advances just past the globally first one.
+    __shared__ int s_pos[4];
+    __shared__ float s_o[4][3];
+    __shared__ int s_gpos;
+    __shared__ float s_nc[3];
+    const int T = team_blocks;
+    const bool coop = team_coop && G > 0;
+    const bool spec = coop && 2 * G <= 64;
+    const int GE = spec ? 2 * G : (G > 0 ? G : 1);
+    const int E = G > 0 ? 64 / GE : 0;
+    int round = 0;
+    for (int s = 0; s < nseg; ++s) {
+      const int start = seg_start[s];
+      const int end = (s + 1 < nseg) ? seg_start[s + 1] : ndep;
+      if (end - start < long_len) continue;
+      const unsigned long long t_seg = __builtin_amdgcn_s_memrealtime();
+      int rounds_here = 0;
+      V3 c = seg_init_carry(dep_key, wcarry, start);
+      int j = start;
+      while (j < end) {
+        // this wave's entries: one per lane, or one per lane group (cooperative)
+        const int per_wave = coop ? E : 64;
+        const int base = j + ((int)blockIdx.x * 4 + wave) * per_wave;
+        const int eslot = coop ? lane / GE : lane;
+        const int idx = base + eslot;
+        const bool valid = (coop ? eslot < E : true) && idx < end;
+        V3 o = c;
+        {
+          int zero = 0;
+          if (valid) {
+            const DepRec rr = dep_rec[idx];
+            if (!coop) o = carry_path(sc, rr, maxrec, c, zero);
+            else if (spec) o = carry_path_spec(sc, ls, lane % G, G, (lane / G) & 1, rr, maxrec, c, zero);
+            else o = carry_path_coop(sc, ls, lane % G, G, rr, maxrec, c, zero);
+          }
+        }
+        const bool lead = coop ? (lane % GE) == 0 : true;
+        const unsigned long long m = __ballot(valid && lead && !same_bits(o, c));
+        const int k = m ? __ffsll((long long)m) - 1 : -1;
+        if (lane == 0) s_pos[wave] = k >= 0 ? base + (coop ? k / GE : k) : 0x7fffffff;
+        if (k >= 0 && lane == k) {
+          s_o[wave][0] = o.x;
+          s_o[wave][1] = o.y;
+          s_o[wave][2] = o.z;
+        }
+        __syncthreads();
+        TeamSlot* slot = &ts->slot[round & 1][blockIdx.x];
+        if (threadIdx.x == 0) {
+          int w = 0;
+          for (int q = 1; q < 4; ++q)
+            if (s_pos[q] < s_pos[w]) w = q;
+          const unsigned pos = (unsigned)s_pos[w];
+          const bool hit = s_pos[w] != 0x7fffffff;
+          __hip_atomic_store(&slot->g0, pack2(pos, hit ? __float_as_uint(s_o[w][0]) : 0u),
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(&slot->g1,
+                             pack2(hit ? __float_as_uint(s_o[w][1]) : 0u,
+                                   hit ? __float_as_uint(s_o[w][2]) : 0u),
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        ++round;
+        ++rounds_here;
+        team_barrier(ts, round * T);
+        // every thread t < T reads slot t; block-wide minimum position
+        {
+          unsigned long long g0 = 0x7fffffffull, g1 = 0;
+          if ((int)threadIdx.x < T) {
+            g0 = __hip_atomic_load(&ts->slot[(round - 1) & 1][threadIdx.x].g0, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            g1 = __hip_atomic_load(&ts->slot[(round - 1) & 1][threadIdx.x].g1, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+          }
+          int pos = (int)(unsigned)g0;
+          int mp = pos;
+          for (int off = 32; off > 0; off >>= 1) {
+            const int u = __shfl_xor(mp, off, 64);
+            mp = u < mp ? u : mp;
+          }
+          if (lane == 0) s_pos[wave] = mp;
+          __syncthreads();
+          const int gmin = min(min(s_pos[0], s_pos[1]), min(s_pos[2], s_pos[3]));
+          if (threadIdx.x == 0) s_gpos = gmin;
+          if (gmin != 0x7fffffff && pos == gmin && (int)threadIdx.x < T) {
+            s_nc[0] = __uint_as_float((unsigned)(g0 >> 32));
+            s_nc[1] = __uint_as_float((unsigned)g1);
+            s_nc[2] = __uint_as_float((unsigned)(g1 >> 32));
+          }
+        }
+        __syncthreads();
+        const int gpos = s_gpos;
+        // entries before the first changer, and the changer itself, read carry c
+        if (valid && idx <= gpos) cin[idx] = make_float4(c.x, c.y, c.z, 0.0f);
+        if (gpos == 0x7fffffff) {
+          j += T * 4 * per_wave;
+        } else {
+          j = gpos + 1;
+          c = v3(s_nc[0], s_nc[1], s_nc[2]);
+        }
+        __syncthreads();
+        if (__hip_atomic_load(&ts->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+      }
+      if (trace && blockIdx.x == 0 && threadIdx.x == 0) {
+        trace[2 * s] = (unsigned)(__builtin_amdgcn_s_memrealtime() - t_seg);
+        trace[2 * s + 1] = (unsigned)rounds_here | 0x80000000u;
+      }
+    }
+    return;
+  }
+
+  // ------------------------------------------------------------- regular waves --
+  for (;;) {
+    int s = 0;
+    if (lane == 0) s = atomicAdd(head, 1);
+    s = __shfl(s, 0, 64);
+    if (s >= nseg) break;
+    const int start = seg_start[s];
+    const int end = (s + 1 < nseg) ? seg_start[s + 1] : ndep;
+    if (team_blocks > 0 && end - start >= long_len) continue;
+    const unsigned long long t_seg = __builtin_amdgcn_s_memrealtime();
+    int iters = 0;
+    V3 c = seg_init_carry(dep_key, wcarry, start);
+    for (int j = start; j < end; j += 64) {
+      V3 mine;
+      iters += wave_window(sc, maxrec, dep_rec, j, end, c, mine, ls, G);
+      if (j + lane < end) cin[j + lane] = make_float4(mine.x, mine.y, mine.z, 0.0f);
+    }
+    if (trace && lane == 0) {
+      trace[2 * s] = (unsigned)(__builtin_amdgcn_s_memrealtime() - t_seg);
+      trace[2 * s + 1] = (unsigned)iters;
+    }
   }
 }
 
@@ -395,26 +685,52 @@ hipError_t launch_parity(const LaunchScene& s, int W, int H, int maxrec, uint8_t
                          hipEvent_t ev_a, hipEvent_t ev_b, hipEvent_t ev_c) {
   const Scene sc = make_scene(s);
   const Cam cam = make_cam(s, W, H);
+  const long long P = (long long)W * H;
   dim3 grid((W + kTile - 1) / kTile, (H + kTile - 1) / kTile);
   hipLaunchKernelGGL(k_phase_a, grid, dim3(kBlock), 0, stream, sc, cam, W, H, maxrec, out,
                      w.cls, w.wcarry, (DepRec*)w.deprec, zcount);
   if (ev_a) (void)hipEventRecord(ev_a, stream);
   (void)hipMemsetAsync(w.counters, 0, 4 * sizeof(int), stream);   // nseg, head, ndep, pad
+  (void)hipMemsetAsync(w.team, 0, 128, stream);                   // arrive, error
   hipLaunchKernelGGL(k_row_stats, dim3(H), dim3(kScanBlock), 0, stream, w.cls, W, w.row_ndep,
                      w.row_lastw, w.row_lastdep);
   hipLaunchKernelGGL(k_row_scan, dim3(1), dim3(1024), 0, stream, H, w.row_ndep, w.row_lastw,
                      w.row_lastdep, w.row_off, w.row_prevw, w.row_prevdep, w.counters + 2);
   hipLaunchKernelGGL(k_row_compact, dim3(H), dim3(kScanBlock), 0, stream, w.cls, W, w.row_off,
-                     w.row_prevw, w.row_prevdep, w.dep_pix, w.dep_key, w.seg_start,
+                     w.row_prevw, w.row_prevdep, (const DepRec*)w.deprec, (DepRec*)w.dep_rec,
+                     w.dep_pix, w.dep_key, w.seg_flag);
+  const int nblk = (int)((P + kFlagBlock - 1) / kFlagBlock);
+  hipLaunchKernelGGL(k_flag_count, dim3(nblk), dim3(kFlagBlock), 0, stream, w.seg_flag,
+                     w.counters + 2, w.blk_cnt);
+  hipLaunchKernelGGL(k_flag_scan, dim3(1), dim3(1024), 0, stream, w.counters + 2, w.blk_cnt,
                      w.counters + 0);
-  hipLaunchKernelGGL(k_resolve, dim3(w.resolve_blocks), dim3(kResolveBlock), 0, stream, sc,
-                     maxrec, w.dep_pix, w.dep_key, (const DepRec*)w.deprec, w.wcarry,
-                     w.seg_start, w.counters + 0, w.counters + 2, w.counters + 1, w.cin);
+  hipLaunchKernelGGL(k_flag_scatter, dim3(nblk), dim3(kFlagBlock), 0, stream, w.seg_flag,
+                     w.counters + 2, w.blk_cnt, w.seg_start);
+  // resolve_lds > 80 KiB keeps one resolver block (4 waves, one per SIMD) per CU: the chain
+  // steps are latency-bound, so a resolver wave should not share its SIMD
+  hipLaunchKernelGGL(k_resolve, dim3(w.resolve_blocks), dim3(kResolveBlock), w.resolve_lds, stream, sc,
+                     maxrec, (const DepRec*)w.dep_rec, w.dep_key, w.wcarry, w.seg_start,
+                     w.counters, w.counters + 1, w.cin, w.team_blocks, w.long_len,
+                     (TeamState*)w.team, w.trace, w.coop_group, w.team_coop);
   if (ev_b) (void)hipEventRecord(ev_b, stream);
   hipLaunchKernelGGL(k_phase_c, dim3(w.phase_c_blocks), dim3(kBlock), 0, stream, sc, cam, W,
                      maxrec, w.dep_pix, w.cin, w.counters + 2, out, zcount);
   if (ev_c) (void)hipEventRecord(ev_c, stream);
   return hipGetLastError();
+}
+
+size_t team_state_bytes() { return sizeof(TeamState); }
+
+int resolve_blocks_resident(int cus, int lds_bytes) {
+  if (lds_bytes > 0)
+    (void)hipFuncSetAttribute((const void*)k_resolve,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_resolve, kResolveBlock,
+                                                   lds_bytes) != hipSuccess ||
+      per_cu <= 0)
+    per_cu = 1;
+  return per_cu * cus;
 }
 
 size_t deprec_bytes() { return sizeof(DepRec); }
