@@ -342,6 +342,7 @@ __global__ void __launch_bounds__(kFlagBlock) k_flag_scatter(const uint8_t* __re
 // device's resident capacity).
 constexpr int kResolveBlock = 256;
 constexpr int kTeamMax = 256;
+constexpr int kLdsShapes = 64;
 
 __device__ __forceinline__ bool same_bits(V3 a, V3 b) {
   return __float_as_uint(a.x) == __float_as_uint(b.x) &&
@@ -443,41 +444,63 @@ __device__ __forceinline__ int wave_window(const Scene& sc, int maxrec,
   return evals;
 }
 
-// 8-byte granules: {first changed wave (-1: none), carry.x}, {carry.y, carry.z}
-struct alignas(16) TeamSlot {
-  unsigned long long g0, g1;
+// Team hand-off by data-tagged 8-byte granules (MI355X_MICROARCH.md: granule hand-off, R2):
+// each block publishes {first changer position, carry x, y, z} as four granules
+// {payload:32, round:32} with agent-scope (sc1) stores; a reader spins on the granules
+// themselves until every tag equals the round, so no counter, fence or drain sits on the
+// path.  Slots are double-buffered by round parity (a block writes round r+1 only after it
+// has read every round-r slot, and nobody reaches round r+2 before everyone read round r+1).
+struct alignas(32) TeamSlot {
+  unsigned long long g[4];
 };
 __device__ __forceinline__ unsigned long long pack2(unsigned lo, unsigned hi) {
   return (unsigned long long)lo | ((unsigned long long)hi << 32);
 }
 
 struct TeamState {
-  int arrive;       // monotonic arrival counter (one add per block per round)
-  int error;        // spin timeout
-  int pad[30];
+  int error;        // a granule spin timed out (5 s)
+  int pad[31];
   TeamSlot slot[2][kTeamMax];
 };
 
-// Counter barrier over the team's blocks.  The hand-off follows MI355X_MICROARCH.md's
-// fence-free row: each block's slot is written by ONE lane with agent-scope (sc1) stores, that
-// lane drains them (s_waitcnt vmcnt(0)) before its agent-scope counter add, and consumers
-// poll the counter and read slots with sc1 loads only.  The spin is bounded (5 s) and
-// reports a timeout through ts->error instead of hanging.
-__device__ __forceinline__ void team_barrier(TeamState* ts, int target) {
-  if (threadIdx.x == 0) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_fetch_add(&ts->arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    while (__hip_atomic_load(&ts->arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-      if (__builtin_amdgcn_s_memrealtime() - t0 > 500000000ull) {   // 5 s at 100 MHz
-        __hip_atomic_store(&ts->error, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-    }
-  }
-  __syncthreads();
+__device__ __forceinline__ void team_publish(TeamState* ts, int round, unsigned pos, V3 c) {
+  TeamSlot* sl = &ts->slot[round & 1][blockIdx.x];
+  const unsigned tag = (unsigned)round;
+  __hip_atomic_store(&sl->g[0], pack2(pos, tag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(&sl->g[1], pack2(__float_as_uint(c.x), tag), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(&sl->g[2], pack2(__float_as_uint(c.y), tag), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(&sl->g[3], pack2(__float_as_uint(c.z), tag), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Spin until block b's round-`round` slot is complete; returns false on timeout.
+__device__ __forceinline__ bool team_collect(TeamState* ts, int round, int b, unsigned& pos,
+                                             V3& c) {
+  TeamSlot* sl = &ts->slot[round & 1][b];
+  const unsigned tag = (unsigned)round;
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  for (;;) {
+    const unsigned long long g0 = __hip_atomic_load(&sl->g[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long g1 = __hip_atomic_load(&sl->g[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long g2 = __hip_atomic_load(&sl->g[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long g3 = __hip_atomic_load(&sl->g[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((unsigned)(g0 >> 32) == tag && (unsigned)(g1 >> 32) == tag &&
+        (unsigned)(g2 >> 32) == tag && (unsigned)(g3 >> 32) == tag) {
+      pos = (unsigned)g0;
+      c = v3(__uint_as_float((unsigned)g1), __uint_as_float((unsigned)g2),
+             __uint_as_float((unsigned)g3));
+      return true;
+    }
+    if (__builtin_amdgcn_s_memrealtime() - t0 > 500000000ull) {
+      __hip_atomic_store(&ts->error, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+  }
+}
+
+template <bool kLds>
 __global__ void __launch_bounds__(kResolveBlock) k_resolve(
     Scene sc, int maxrec, const DepRec* __restrict__ dep_rec,
     const long long* __restrict__ dep_key, const float4* __restrict__ wcarry,
@@ -487,6 +510,17 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
   const int nseg = counters[0];
   const int ndep = counters[2];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // The chain steps read the winner's record (hit_frame) and refl[obj] every bounce level:
+  // stage the shape records (n <= kLdsShapes) in LDS so those reads cost an LDS access
+  // instead of a vector-memory round trip.
+  __shared__ rc_shape s_shapes[kLds ? kLdsShapes + 1 : 1];
+  if (kLds) {   // host guarantees n <= kLdsShapes
+    const int words = (int)(sizeof(rc_shape) / 4) * (sc.n + 1);
+    for (int i = threadIdx.x; i < words; i += blockDim.x)
+      ((unsigned*)s_shapes)[i] = ((const unsigned*)sc.shapes)[i];
+    __syncthreads();
+    sc.shapes = s_shapes;
+  }
   LaneShape ls;
   ls.has = false;
   if (G > 0) {
@@ -544,33 +578,24 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
           s_o[wave][2] = o.z;
         }
         __syncthreads();
-        TeamSlot* slot = &ts->slot[round & 1][blockIdx.x];
+        ++round;
+        ++rounds_here;
         if (threadIdx.x == 0) {
           int w = 0;
           for (int q = 1; q < 4; ++q)
             if (s_pos[q] < s_pos[w]) w = q;
-          const unsigned pos = (unsigned)s_pos[w];
           const bool hit = s_pos[w] != 0x7fffffff;
-          __hip_atomic_store(&slot->g0, pack2(pos, hit ? __float_as_uint(s_o[w][0]) : 0u),
-                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_store(&slot->g1,
-                             pack2(hit ? __float_as_uint(s_o[w][1]) : 0u,
-                                   hit ? __float_as_uint(s_o[w][2]) : 0u),
-                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          team_publish(ts, round, (unsigned)s_pos[w],
+                       hit ? v3(s_o[w][0], s_o[w][1], s_o[w][2]) : v3(0.0f, 0.0f, 0.0f));
         }
-        ++round;
-        ++rounds_here;
-        team_barrier(ts, round * T);
-        // every thread t < T reads slot t; block-wide minimum position
+        // every thread t < T collects slot t; block-wide minimum position
         {
-          unsigned long long g0 = 0x7fffffffull, g1 = 0;
-          if ((int)threadIdx.x < T) {
-            g0 = __hip_atomic_load(&ts->slot[(round - 1) & 1][threadIdx.x].g0, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-            g1 = __hip_atomic_load(&ts->slot[(round - 1) & 1][threadIdx.x].g1, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-          }
-          int pos = (int)(unsigned)g0;
+          unsigned upos = 0x7fffffffu;
+          V3 oc = v3(0.0f, 0.0f, 0.0f);
+          bool ok = true;
+          if ((int)threadIdx.x < T) ok = team_collect(ts, round, threadIdx.x, upos, oc);
+          if (__syncthreads_or(!ok)) return;
+          const int pos = (int)upos;
           int mp = pos;
           for (int off = 32; off > 0; off >>= 1) {
             const int u = __shfl_xor(mp, off, 64);
@@ -581,9 +606,9 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
           const int gmin = min(min(s_pos[0], s_pos[1]), min(s_pos[2], s_pos[3]));
           if (threadIdx.x == 0) s_gpos = gmin;
           if (gmin != 0x7fffffff && pos == gmin && (int)threadIdx.x < T) {
-            s_nc[0] = __uint_as_float((unsigned)(g0 >> 32));
-            s_nc[1] = __uint_as_float((unsigned)g1);
-            s_nc[2] = __uint_as_float((unsigned)(g1 >> 32));
+            s_nc[0] = oc.x;
+            s_nc[1] = oc.y;
+            s_nc[2] = oc.z;
           }
         }
         __syncthreads();
@@ -597,7 +622,6 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
           c = v3(s_nc[0], s_nc[1], s_nc[2]);
         }
         __syncthreads();
-        if (__hip_atomic_load(&ts->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
       }
       if (trace && blockIdx.x == 0 && threadIdx.x == 0) {
         trace[2 * s] = (unsigned)(__builtin_amdgcn_s_memrealtime() - t_seg);
@@ -691,7 +715,7 @@ hipError_t launch_parity(const LaunchScene& s, int W, int H, int maxrec, uint8_t
                      w.cls, w.wcarry, (DepRec*)w.deprec, zcount);
   if (ev_a) (void)hipEventRecord(ev_a, stream);
   (void)hipMemsetAsync(w.counters, 0, 4 * sizeof(int), stream);   // nseg, head, ndep, pad
-  (void)hipMemsetAsync(w.team, 0, 128, stream);                   // arrive, error
+  (void)hipMemsetAsync(w.team, 0, sizeof(TeamState), stream);     // error + round tags
   hipLaunchKernelGGL(k_row_stats, dim3(H), dim3(kScanBlock), 0, stream, w.cls, W, w.row_ndep,
                      w.row_lastw, w.row_lastdep);
   hipLaunchKernelGGL(k_row_scan, dim3(1), dim3(1024), 0, stream, H, w.row_ndep, w.row_lastw,
@@ -708,7 +732,8 @@ hipError_t launch_parity(const LaunchScene& s, int W, int H, int maxrec, uint8_t
                      w.counters + 2, w.blk_cnt, w.seg_start);
   // resolve_lds > 80 KiB keeps one resolver block (4 waves, one per SIMD) per CU: the chain
   // steps are latency-bound, so a resolver wave should not share its SIMD
-  hipLaunchKernelGGL(k_resolve, dim3(w.resolve_blocks), dim3(kResolveBlock), w.resolve_lds, stream, sc,
+  auto kres = s.n <= kLdsShapes ? k_resolve<true> : k_resolve<false>;
+  hipLaunchKernelGGL(kres, dim3(w.resolve_blocks), dim3(kResolveBlock), w.resolve_lds, stream, sc,
                      maxrec, (const DepRec*)w.dep_rec, w.dep_key, w.wcarry, w.seg_start,
                      w.counters, w.counters + 1, w.cin, w.team_blocks, w.long_len,
                      (TeamState*)w.team, w.trace, w.coop_group, w.team_coop);
@@ -722,11 +747,14 @@ hipError_t launch_parity(const LaunchScene& s, int W, int H, int maxrec, uint8_t
 size_t team_state_bytes() { return sizeof(TeamState); }
 
 int resolve_blocks_resident(int cus, int lds_bytes) {
-  if (lds_bytes > 0)
-    (void)hipFuncSetAttribute((const void*)k_resolve,
+  if (lds_bytes > 0) {
+    (void)hipFuncSetAttribute((const void*)k_resolve<true>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
+    (void)hipFuncSetAttribute((const void*)k_resolve<false>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
+  }
   int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_resolve, kResolveBlock,
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_resolve<true>, kResolveBlock,
                                                    lds_bytes) != hipSuccess ||
       per_cu <= 0)
     per_cu = 1;
