@@ -1,21 +1,25 @@
 #!/usr/bin/env python3
-"""Benchmark: primary rays/s (= pixels/s) rendering quadric.scene at 4096x4096, depth 6
+"""Benchmark: primary rays/s (= pixels/s) rendering quadric.scene at 4096x4096, bounce depth 6
 (MAX_RECURSION 7, C/raycast.c:14) — BASELINE.json's metric.
 
-A "step" is one full render of the image through the C-ABI (rc_render_device): scene
-already resident in HBM, output written to a device buffer, every kernel of the mode
-inside the timed region (parity mode: phase A + compaction + carry resolver + phase C).
+A "step" is one full render of the image through the C-ABI (rc_render_device): scene already
+resident in HBM, output written to a device buffer, every kernel of the mode inside the
+timed region.  Parity mode (default, byte-identical to the reference): phase A + scan-order
+compaction + carry-chain resolver + phase C.  Fast mode: one render kernel.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--mode parity|fast]
 
-N > 1 (torchrun, one rank per GPU): rows are dealt cyclically (row r -> rank r mod N), each
-rank renders its rows, and the row blocks are gathered to rank 0 over RCCL (torch.distributed
-"nccl" backend) and de-interleaved there — inside the timed region.  Parity mode at N > 1
-needs the whole scan-order carry chain: see DESIGN.md §multi-GPU.
+Multi-GPU (torchrun, one rank per GPU, RANK/LOCAL_RANK/WORLD_SIZE from the env):
+  parity: the image's scan-order carry chain is one serial dependency,
+          so the path does not shard: every rank renders its own full image (replicas, no
+          data-path collective) and `value` = N images' pixels / max rank time ("weak").
+  fast:   rows dealt cyclically (row r -> rank r mod N), each rank renders its rows, the row
+          blocks are gathered over RCCL (all_gather_into_tensor, "nccl" backend) and
+          de-interleaved on rank 0 inside the timed region ("strong").
 
-Rank 0 prints one JSON line (contract in the task statement) with a `roofline` object for
-the dominant kernel (timed live with HIP events) and a `cpu_baseline` object (the reference
-C/ build from oracle/_ref, timed on this host on one core; N=1 only).
+Rank 0 prints one JSON line with `roofline` (the dominant kernel, timed live with HIP events
+on its stream through rc_profile_begin/end), per-phase times and `cpu_baseline` (the reference
+C/ build from oracle/_ref on one host core; N=1 only).
 """
 import argparse
 import importlib.util
@@ -27,11 +31,16 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 
-# Algorithmic work per pixel (SURVEY.md §8d weights applied to the oracle's exact per-pixel
-# counts at this config; derivation in DESIGN.md §roofline).
-FLOP_PER_PX = {"quadric:4096:6": 1380.0}
+# Algorithmic work: SURVEY.md §8d's per-operation weights (sphere test
+# 29, plane 15, quadric 81, hit post-processing ~26, light setup 18, unshadowed light 70,
+# reflect+normalize 21, ray generation 15) applied to the exact per-pixel work counts of
+# the reference at this config (oracle counters, quadric 4096^2 depth 6).
+WORK = {
+    "quadric:4096:6": {"render_flop_per_px": 1374.0,   # full render, every pixel
+                       "dep_flop_per_entry": 1618.0},  # one carry transfer function
+}
 PEAK_FP64_TFLOPS = 78.6    # MI355X vector FP64 (MI355X_MICROARCH.md: FP32 157.3 / 2)
-PEAK_HBM_GBS = 8000.0
+PEAK_HBM_GBS = 8000.0      # MI355X HBM3E
 
 
 def load_pkg():
@@ -45,10 +54,10 @@ def load_pkg():
 
 
 def cpu_baseline(scene_path, size, depth):
-    """The reference itself (oracle/_ref/ref_timer_d<depth>: C/ sources, gcc -O3) rendering the
-    same image on one host core; falls back to the CPU restatement (oracle/build)."""
+    """The reference itself (oracle/_ref/ref_timer_d<depth>: the C/ sources built like
+    C/Makefile:4, raycast() timed alone) on the same image on one pinned host core; falls
+    back to the CPU restatement (oracle/build) when the reference build is absent."""
     ref = os.path.join(ROOT, "oracle", "_ref", f"ref_timer_d{depth}")
-    env = dict(os.environ, OMP_NUM_THREADS="1")
     if os.path.exists(ref):
         cmd, kind = [ref, str(size), str(size), scene_path], "reference"
     else:
@@ -56,14 +65,16 @@ def cpu_baseline(scene_path, size, depth):
                scene_path, "/dev/null", str(depth)]
         kind = "port"
     try:
-        cmd = ["taskset", "-c", "0"] + cmd
-        out = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env,
-                             check=True).stdout
-        line = [l for l in out.splitlines() if l.startswith("{")][-1]
-        r = json.loads(line)
+        try:
+            core = sorted(os.sched_getaffinity(0))[0]
+            cmd = ["taskset", "-c", str(core)] + cmd
+        except (AttributeError, OSError):
+            pass
+        out = subprocess.run(cmd, capture_output=True, text=True, timeout=300, check=True).stdout
+        r = json.loads([l for l in out.splitlines() if l.startswith("{")][-1])
         return {"value": round(r["rays_per_s"], 1), "unit": "rays/s", "cores": 1, "kind": kind,
-                "sample": f"full {size}x{size} quadric.scene d{depth} render, raycast() only, "
-                          f"1 pinned core ({r['seconds']:.2f} s)"}
+                "sample": f"full {size}x{size} quadric.scene depth {depth} render, raycast() "
+                          f"only, 1 pinned core: {r['seconds']:.2f} s"}
     except Exception as e:  # noqa: BLE001
         return {"value": None, "unit": "rays/s", "cores": 1, "kind": kind, "sample": f"failed: {e}"}
 
@@ -94,26 +105,29 @@ def main():
     scene = pkg.Scene.from_file(scene_path)
     W = H = args.size
     mode = args.mode
-    if world > 1 and mode == "parity":
-        mode = "fast"   # the carry chain is not sharded yet
-    nrows = (H - rank + world - 1) // world
+    sharded = world > 1 and mode == "fast"
+    if sharded:
+        row0, step_rows, nrows = pkg.row_shard(H, rank, world)
+    else:
+        row0, step_rows, nrows = 0, 1, H
     out = torch.empty((nrows, W, 3), dtype=torch.uint8, device="cuda")
-    gathered = (torch.empty((world, (H + world - 1) // world, W, 3), dtype=torch.uint8,
-                            device="cuda") if world > 1 else None)
-    full = torch.empty((H, W, 3), dtype=torch.uint8, device="cuda") if world > 1 else None
     stream = torch.cuda.current_stream()
+    if sharded:
+        rows_max = (H + world - 1) // world
+        gathered = torch.empty((world, rows_max, W, 3), dtype=torch.uint8, device="cuda")
+        send = torch.zeros((rows_max, W, 3), dtype=torch.uint8, device="cuda")
+        full = torch.empty((rows_max * world, W, 3), dtype=torch.uint8, device="cuda")
 
     def step():
-        pkg.render_device(scene, W, H, out.data_ptr(), stream.cuda_stream, depth=args.depth,
-                          mode=mode, row0=rank, row_step=world, nrows=nrows)
-        if world > 1:
-            send = out
-            pad = gathered.shape[1] - nrows
-            if pad:
-                send = torch.cat([out, out.new_zeros((pad, W, 3))])
-            dist.all_gather_into_tensor(gathered, send)
-            if rank == 0:   # row y lives in rank y % N at local row y // N
-                full.copy_(gathered.permute(1, 0, 2, 3).reshape(-1, W, 3)[:H])
+        if sharded:
+            pkg.render_device(scene, W, H, send.data_ptr(), stream.cuda_stream, depth=args.depth,
+                              mode=mode, row0=row0, row_step=step_rows, nrows=nrows)
+            pkg.gather_rows(send, gathered, dist)
+            if rank == 0:   # image row y lives on rank y % N at local row y // N
+                full.copy_(pkg.deinterleave(gathered, rows_max * world))
+        else:
+            pkg.render_device(scene, W, H, out.data_ptr(), stream.cuda_stream, depth=args.depth,
+                              mode=mode)
 
     for _ in range(args.warmup):
         step()
@@ -121,7 +135,7 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    kernel_ms = []
+    pkg.profile_begin()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -130,23 +144,33 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    phases = pkg.profile_end()
     tmax = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
     if world > 1:
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
     tmax = float(tmax.item())
 
-    # live kernel timing of the dominant kernel (HIP events on its stream, inside the lib)
     tim = {}
-    pkg.render_device(scene, W, H, out.data_ptr(), stream.cuda_stream, depth=args.depth,
-                      mode=mode, row0=rank, row_step=world, nrows=nrows, timing=tim)
+    pkg.render_device(scene, W, H, (send if sharded else out).data_ptr(), stream.cuda_stream,
+                      depth=args.depth, mode=mode, row0=row0, row_step=step_rows, nrows=nrows,
+                      timing=tim)
     torch.cuda.synchronize()
     if rank == 0:
-        value = W * H * args.steps / tmax
-        key = f"{args.scene}:{args.size}:{args.depth}"
-        flop_px = FLOP_PER_PX.get(key)
-        main_ms = pkg.last_kernel_ms()   # phase A (parity) or k_render (fast)
-        main_px = W * nrows
-        achieved = (flop_px * main_px / (main_ms * 1e-3) / 1e12) if flop_px and main_ms else None
+        images = 1 if sharded else world
+        value = images * W * H * args.steps / tmax
+        work = WORK.get(f"{args.scene}:{args.size}:{args.depth}")
+        parity = mode == "parity" and args.depth > 0
+        if parity:
+            dom_name, dom_ms = "k_resolve", phases["resolve_ms"]
+            dom_flop = work["dep_flop_per_entry"] * tim["dep_pixels"] if work else None
+            render_ms = phases["phase_a_ms"] + phases["phase_c_ms"]
+        else:
+            dom_name, dom_ms = "k_render", phases["render_ms"]
+            dom_flop = work["render_flop_per_px"] * W * nrows if work else None
+            render_ms = phases["render_ms"]
+        ach = dom_flop / (dom_ms * 1e-3) / 1e12 if dom_flop and dom_ms else None
+        rach = (work["render_flop_per_px"] * W * nrows / (render_ms * 1e-3) / 1e12
+                if work and render_ms else None)
         line = {
             "metric": "primary rays/sec (= pixels/sec) at 4096x4096, quadric.scene",
             "value": round(value, 1),
@@ -156,26 +180,36 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(tmax * 1e3 / args.steps, 4),
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": "strong" if sharded else "weak",
             "vs_baseline": None,
             "dtype": "f32+f64",
-            "data": "synthetic: the reference's own examples/quadric.scene",
-            "config": {"workload": f"{args.scene}.scene {W}x{H} depth {args.depth} "
-                                   f"(MAX_RECURSION {args.depth + 1}), mode {mode}",
+            "data": "synthetic: the reference's own examples/quadric.scene (no dataset)",
+            "config": {"workload": f"{args.scene}.scene {W}x{H}, bounce depth {args.depth} "
+                                   f"(MAX_RECURSION {args.depth + 1}), {mode} mode"
+                                   + (", byte-identical to C/raycast.c" if mode == "parity" else ""),
                        "mode": mode, "width": W, "height": H, "depth": args.depth,
-                       "parallelism": f"rows-cyclic x{world}"},
-            "phases_ms": {k: round(v, 4) for k, v in tim.items() if k.endswith("_ms")},
+                       "parallelism": (f"rows-cyclic x{world} + RCCL all_gather" if sharded else
+                                       (f"replicas x{world}" if world > 1 else "single GPU"))},
+            "phases_ms": {k: round(v, 4) for k, v in phases.items() if k.endswith("_ms")},
             "dep_pixels": tim.get("dep_pixels"),
-            "roofline": {"bound": "valu", "kernel": "k_phase_a" if mode == "parity" else "k_render",
-                         "achieved": round(achieved, 3) if achieved else None,
+            "roofline": {"bound": "valu", "kernel": dom_name,
+                         "kernel_ms": round(dom_ms, 4),
+                         "achieved": round(ach, 4) if ach else None,
                          "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(achieved / PEAK_FP64_TFLOPS, 5) if achieved else None,
-                         "traffic": None},
-            "roofline_hbm": {"bound": "hbm", "kernel": "framebuffer store",
-                             "achieved": round(3 * W * H / (tmax / args.steps) / 1e9, 3),
-                             "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                             "frac": round(3 * W * H / (tmax / args.steps) / 1e9 / PEAK_HBM_GBS, 6),
-                             "traffic": None},
+                         "frac": round(ach / PEAK_FP64_TFLOPS, 5) if ach else None,
+                         "traffic": None,
+                         "note": ("serial carry chain: latency-bound, see DESIGN.md" if parity
+                                  else "throughput kernel")},
+            "roofline_render": {"bound": "valu",
+                                "kernel": "k_phase_a+k_phase_c" if parity else "k_render",
+                                "kernel_ms": round(render_ms, 4),
+                                "achieved": round(rach, 3) if rach else None,
+                                "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
+                                "frac": round(rach / PEAK_FP64_TFLOPS, 4) if rach else None},
+            "roofline_hbm": {"bound": "hbm", "kernel": "framebuffer store (3 B/pixel)",
+                             "achieved": round(3 * W * nrows / (phases["total_ms"] * 1e-3) / 1e9, 3)
+                             if phases["total_ms"] else None,
+                             "peak": PEAK_HBM_GBS, "unit": "GB/s"},
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(scene_path, args.size, args.depth)

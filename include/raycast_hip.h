@@ -171,9 +171,25 @@ int rc_render_device(const rc_scene *scene, int width, int height, int row0, int
                      int nrows, const rc_options *opt, uint8_t *d_out, void *stream,
                      rc_timing *timing);
 
-/* Average duration (ms) of the last rc_render_device() call's main shading kernel,
- * measured with HIP events on its stream. */
+/* Duration (ms) of the last call's dominant kernel on the current device (the carry
+ * resolver in parity mode, the render kernel otherwise), from HIP events on its stream. */
 double rc_last_kernel_ms(void);
+
+/* Per-phase kernel timing averaged over every render of the current device issued between
+ * rc_profile_begin() and rc_profile_end() (HIP events on the render stream; no extra
+ * synchronisation inside the window; at most 64 calls are kept). */
+typedef struct rc_phase_stats {
+  int calls;
+  int parity;
+  double phase_a_ms;    /* parity: phase A (all pixels, first-bounce-miss pixels deferred) */
+  double compact_ms;    /* parity: scan-order DEP compaction + segment table               */
+  double resolve_ms;    /* parity: carry-chain resolver                                    */
+  double phase_c_ms;    /* parity: shading of the deferred pixels                          */
+  double render_ms;     /* fast / depth 0: the single render kernel                        */
+  double total_ms;      /* first kernel start to last kernel end                           */
+} rc_phase_stats;
+int rc_profile_begin(void);
+int rc_profile_end(rc_phase_stats *out);
 
 /* Library version / build string. */
 const char *rc_version(void);

@@ -60,7 +60,12 @@ struct DevCtx {
   int device = 0;
   int cus = 256;
   hipStream_t stream = nullptr;
-  hipEvent_t ev[5] = {};
+  // event sets: [0] start, then per phase ends (fast: [1] = render; parity: [1] phase A,
+  // [2] compaction, [3] resolver, [4] phase C).  Set 0 serves plain calls; inside an
+  // rc_profile_begin/end window every call takes the next set of the pool.
+  static constexpr int kEvSets = 64;
+  hipEvent_t ev[kEvSets][5] = {};
+  int prof_active = 0, prof_calls = 0, prof_parity = 0;
   DevBuf out;          // rc_render output pixmap
   DevBuf zcount;       // zero-normalize counter
   DevBuf scene;        // uploaded packed scene
@@ -88,7 +93,8 @@ int ctx_get(int device, DevCtx** out) {
     HIP_TRY(hipGetDeviceProperties(&prop, device));
     c.cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
     HIP_TRY(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
-    for (auto& e : c.ev) HIP_TRY(hipEventCreate(&e));
+    for (auto& set : c.ev)
+      for (auto& e : set) HIP_TRY(hipEventCreate(&e));
     if (c.zcount.ensure(64)) return -1;
     c.device = device;
     c.init = true;
@@ -244,10 +250,16 @@ int enqueue_render(DevCtx& c, const rc_scene* s, int W, int H, int row0, int row
   HIP_TRY(hipMemsetAsync(zc, 0, sizeof(unsigned long long), stream));
   const int maxrec = opt->max_recursion;
   const bool parity = opt->mode == RC_MODE_PARITY && maxrec > 1;
-  if (timed) HIP_TRY(hipEventRecord(c.ev[0], stream));
+  hipEvent_t* ev = c.ev[0];
+  if (c.prof_active) {
+    ev = c.ev[c.prof_calls % DevCtx::kEvSets];
+    c.prof_calls++;
+    c.prof_parity = parity;
+  }
+  if (timed) HIP_TRY(hipEventRecord(ev[0], stream));
   if (!parity) {
     HIP_TRY(rc::launch_render(ls, W, H, row0, row_step, nrows, maxrec, d_out, zc, stream));
-    if (timed) HIP_TRY(hipEventRecord(c.ev[1], stream));
+    if (timed) HIP_TRY(hipEventRecord(ev[1], stream));
     return 0;
   }
   if (row0 != 0 || row_step != 1 || nrows != H) {
@@ -259,8 +271,7 @@ int enqueue_render(DevCtx& c, const rc_scene* s, int W, int H, int row0, int row
     std::fprintf(stderr, "Error: out of device memory for the parity workspace\n");
     return -1;
   }
-  HIP_TRY(rc::launch_parity(ls, W, H, maxrec, d_out, w, zc, stream, timed ? c.ev[1] : nullptr,
-                            timed ? c.ev[2] : nullptr, timed ? c.ev[3] : nullptr));
+  HIP_TRY(rc::launch_parity(ls, W, H, maxrec, d_out, w, zc, stream, timed ? ev + 1 : nullptr));
   return 0;
 }
 
@@ -272,11 +283,12 @@ double event_ms(hipEvent_t a, hipEvent_t b) {
 
 void fill_device_timing(DevCtx& c, const rc_options* opt, rc_timing* t) {
   const bool parity = opt->mode == RC_MODE_PARITY && opt->max_recursion > 1;
-  double k = parity ? event_ms(c.ev[0], c.ev[3]) : event_ms(c.ev[0], c.ev[1]);
-  g_last_kernel_ms = parity ? event_ms(c.ev[0], c.ev[1]) : k;
+  hipEvent_t* ev = c.ev[0];
+  double k = parity ? event_ms(ev[0], ev[4]) : event_ms(ev[0], ev[1]);
+  g_last_kernel_ms = parity ? event_ms(ev[2], ev[3]) : k;
   if (!t) return;
   t->kernel_ms = k;
-  t->resolve_ms = parity ? event_ms(c.ev[1], c.ev[2]) : 0.0;
+  t->resolve_ms = parity ? event_ms(ev[2], ev[3]) : 0.0;
   unsigned long long z = 0;
   if (hipMemcpy(&z, c.zcount.p, sizeof z, hipMemcpyDeviceToHost) == hipSuccess)
     t->zero_normalize = (int64_t)z;
@@ -333,6 +345,51 @@ int rc_render_device(const rc_scene* s, int W, int H, int row0, int row_step, in
     HIP_TRY(hipStreamSynchronize(st));
     fill_device_timing(*c, opt, timing);
     timing->total_ms = timing->kernel_ms;
+  }
+  return 0;
+}
+
+int rc_profile_begin(void) {
+  int dev = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  DevCtx* c;
+  if (ctx_get(dev, &c)) return -1;
+  c->prof_active = 1;
+  c->prof_calls = 0;
+  return 0;
+}
+
+int rc_profile_end(rc_phase_stats* out) {
+  int dev = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  DevCtx* c;
+  if (ctx_get(dev, &c)) return -1;
+  c->prof_active = 0;
+  std::memset(out, 0, sizeof *out);
+  const int n = c->prof_calls < DevCtx::kEvSets ? c->prof_calls : DevCtx::kEvSets;
+  out->calls = n;
+  out->parity = c->prof_parity;
+  for (int i = 0; i < n; ++i) {
+    hipEvent_t* ev = c->ev[i];
+    HIP_TRY(hipEventSynchronize(ev[c->prof_parity ? 4 : 1]));
+    if (c->prof_parity) {
+      out->phase_a_ms += event_ms(ev[0], ev[1]);
+      out->compact_ms += event_ms(ev[1], ev[2]);
+      out->resolve_ms += event_ms(ev[2], ev[3]);
+      out->phase_c_ms += event_ms(ev[3], ev[4]);
+      out->total_ms += event_ms(ev[0], ev[4]);
+    } else {
+      out->render_ms += event_ms(ev[0], ev[1]);
+      out->total_ms += event_ms(ev[0], ev[1]);
+    }
+  }
+  if (n > 0) {
+    out->phase_a_ms /= n;
+    out->compact_ms /= n;
+    out->resolve_ms /= n;
+    out->phase_c_ms /= n;
+    out->render_ms /= n;
+    out->total_ms /= n;
   }
   return 0;
 }

@@ -54,7 +54,7 @@ hipError_t launch_render(const LaunchScene& s, int W, int H, int row0, int row_s
 
 hipError_t launch_parity(const LaunchScene& s, int W, int H, int maxrec, uint8_t* out,
                          const ParityWork& w, unsigned long long* zcount, hipStream_t stream,
-                         hipEvent_t ev_a, hipEvent_t ev_b, hipEvent_t ev_c);
+                         const hipEvent_t* ev);
 
 size_t deprec_bytes();
 size_t team_state_bytes();

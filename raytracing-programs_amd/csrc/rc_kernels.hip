@@ -706,14 +706,16 @@ hipError_t launch_render(const LaunchScene& s, int W, int H, int row0, int row_s
 
 hipError_t launch_parity(const LaunchScene& s, int W, int H, int maxrec, uint8_t* out,
                          const ParityWork& w, unsigned long long* zcount, hipStream_t stream,
-                         hipEvent_t ev_a, hipEvent_t ev_b, hipEvent_t ev_c) {
+                         const hipEvent_t* ev) {
+  // ev (optional): [0] after phase A, [1] after compaction, [2] after the resolver,
+  // [3] after phase C
   const Scene sc = make_scene(s);
   const Cam cam = make_cam(s, W, H);
   const long long P = (long long)W * H;
   dim3 grid((W + kTile - 1) / kTile, (H + kTile - 1) / kTile);
   hipLaunchKernelGGL(k_phase_a, grid, dim3(kBlock), 0, stream, sc, cam, W, H, maxrec, out,
                      w.cls, w.wcarry, (DepRec*)w.deprec, zcount);
-  if (ev_a) (void)hipEventRecord(ev_a, stream);
+  if (ev) (void)hipEventRecord(ev[0], stream);
   (void)hipMemsetAsync(w.counters, 0, 4 * sizeof(int), stream);   // nseg, head, ndep, pad
   (void)hipMemsetAsync(w.team, 0, sizeof(TeamState), stream);     // error + round tags
   hipLaunchKernelGGL(k_row_stats, dim3(H), dim3(kScanBlock), 0, stream, w.cls, W, w.row_ndep,
@@ -732,15 +734,16 @@ hipError_t launch_parity(const LaunchScene& s, int W, int H, int maxrec, uint8_t
                      w.counters + 2, w.blk_cnt, w.seg_start);
   // resolve_lds > 80 KiB keeps one resolver block (4 waves, one per SIMD) per CU: the chain
   // steps are latency-bound, so a resolver wave should not share its SIMD
+  if (ev) (void)hipEventRecord(ev[1], stream);
   auto kres = s.n <= kLdsShapes ? k_resolve<true> : k_resolve<false>;
   hipLaunchKernelGGL(kres, dim3(w.resolve_blocks), dim3(kResolveBlock), w.resolve_lds, stream, sc,
                      maxrec, (const DepRec*)w.dep_rec, w.dep_key, w.wcarry, w.seg_start,
                      w.counters, w.counters + 1, w.cin, w.team_blocks, w.long_len,
                      (TeamState*)w.team, w.trace, w.coop_group, w.team_coop);
-  if (ev_b) (void)hipEventRecord(ev_b, stream);
+  if (ev) (void)hipEventRecord(ev[2], stream);
   hipLaunchKernelGGL(k_phase_c, dim3(w.phase_c_blocks), dim3(kBlock), 0, stream, sc, cam, W,
                      maxrec, w.dep_pix, w.cin, w.counters + 2, out, zcount);
-  if (ev_c) (void)hipEventRecord(ev_c, stream);
+  if (ev) (void)hipEventRecord(ev[3], stream);
   return hipGetLastError();
 }
 
