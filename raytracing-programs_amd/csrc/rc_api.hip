@@ -234,7 +234,7 @@ int ensure_parity(DevCtx& c, int W, int H, rc::ParityWork& w) {
   }
   w.trace = nullptr;
   if (std::getenv("RC_RESOLVE_TRACE")) {
-    if (c.trace.ensure(P * 2 * sizeof(unsigned))) return -1;
+    if (c.trace.ensure(P * 3 * sizeof(unsigned))) return -1;
     w.trace = (unsigned*)c.trace.p;
   }
   w.phase_c_blocks = c.cus * 8;
@@ -299,16 +299,16 @@ void fill_device_timing(DevCtx& c, const rc_options* opt, rc_timing* t) {
     const char* path = std::getenv("RC_RESOLVE_TRACE");
     if (path && c.trace.p && cnt[0] > 0) {   // debug: per-segment resolver trace
       std::vector<int> starts(cnt[0]);
-      std::vector<unsigned> tr(2 * (size_t)cnt[0]);
+      std::vector<unsigned> tr(3 * (size_t)cnt[0]);
       (void)hipMemcpy(starts.data(), c.seg_start.p, starts.size() * sizeof(int),
                       hipMemcpyDeviceToHost);
       (void)hipMemcpy(tr.data(), c.trace.p, tr.size() * sizeof(unsigned), hipMemcpyDeviceToHost);
       if (FILE* f = std::fopen(path, "w")) {
-        std::fprintf(f, "# seg start len ticks_100MHz evals(team: rounds|0x80000000)\n");
+        std::fprintf(f, "# seg start len ticks_100MHz evals(team: rounds|0x80000000) cycles\n");
         for (int k = 0; k < cnt[0]; ++k) {
           const int end = k + 1 < cnt[0] ? starts[k + 1] : cnt[2];
-          std::fprintf(f, "%d %d %d %u %u\n", k, starts[k], end - starts[k], tr[2 * k],
-                       tr[2 * k + 1]);
+          std::fprintf(f, "%d %d %d %u %u %u\n", k, starts[k], end - starts[k], tr[3 * k],
+                       tr[3 * k + 1], tr[3 * k + 2]);
         }
         std::fclose(f);
       }

@@ -531,65 +531,64 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
 
   if ((int)blockIdx.x < team_blocks) {
     // ------------------------------------------------------------------- team --
-    // One round = every member wave evaluates its 64 entries once at the current carry and
-    // reports its first changer; the team advances just past the globally first one.
+    // Changers inside long segments come in dense clusters separated by long clean runs
+    // (4096^2 quadric: median gap 3 entries, but two runs of 707k and 112k).  The team
+    // alternates two modes:
+    //   SCAN     every team wave evaluates 64 entries, one per lane, at the current carry
+    //            (a T*256-entry window per round); the team agrees on the first changer
+    //            through tagged granules;
+    //   RESOLVE  the leader wave (block 0, wave 0) resolves the cluster that starts there on
+    //            its own (wave_window: per-lane pass + cooperative inner loop, no team sync)
+    //            until a whole 64-entry window comes back clean, then hands (position, carry)
+    //            back to the team.
     __shared__ int s_pos[4];
     __shared__ float s_o[4][3];
     __shared__ int s_gpos;
     __shared__ float s_nc[3];
     const int T = team_blocks;
-    const bool coop = team_coop && G > 0;
-    const bool spec = coop && 2 * G <= 64;
-    const int GE = spec ? 2 * G : (G > 0 ? G : 1);
-    const int E = G > 0 ? 64 / GE : 0;
+    const int window = T * 4 * 64;
     int round = 0;
     for (int s = 0; s < nseg; ++s) {
       const int start = seg_start[s];
       const int end = (s + 1 < nseg) ? seg_start[s + 1] : ndep;
       if (end - start < long_len) continue;
       const unsigned long long t_seg = __builtin_amdgcn_s_memrealtime();
+      const unsigned long long c_seg = __builtin_amdgcn_s_memtime();
       int rounds_here = 0;
       V3 c = seg_init_carry(dep_key, wcarry, start);
       int j = start;
+      bool resolve = false;
       while (j < end) {
-        // this wave's entries: one per lane, or one per lane group (cooperative)
-        const int per_wave = coop ? E : 64;
-        const int base = j + ((int)blockIdx.x * 4 + wave) * per_wave;
-        const int eslot = coop ? lane / GE : lane;
-        const int idx = base + eslot;
-        const bool valid = (coop ? eslot < E : true) && idx < end;
-        V3 o = c;
-        {
-          int zero = 0;
-          if (valid) {
-            const DepRec rr = dep_rec[idx];
-            if (!coop) o = carry_path(sc, rr, maxrec, c, zero);
-            else if (spec) o = carry_path_spec(sc, ls, lane % G, G, (lane / G) & 1, rr, maxrec, c, zero);
-            else o = carry_path_coop(sc, ls, lane % G, G, rr, maxrec, c, zero);
-          }
-        }
-        const bool lead = coop ? (lane % GE) == 0 : true;
-        const unsigned long long m = __ballot(valid && lead && !same_bits(o, c));
-        const int k = m ? __ffsll((long long)m) - 1 : -1;
-        if (lane == 0) s_pos[wave] = k >= 0 ? base + (coop ? k / GE : k) : 0x7fffffff;
-        if (k >= 0 && lane == k) {
-          s_o[wave][0] = o.x;
-          s_o[wave][1] = o.y;
-          s_o[wave][2] = o.z;
-        }
-        __syncthreads();
         ++round;
         ++rounds_here;
-        if (threadIdx.x == 0) {
-          int w = 0;
-          for (int q = 1; q < 4; ++q)
-            if (s_pos[q] < s_pos[w]) w = q;
-          const bool hit = s_pos[w] != 0x7fffffff;
-          team_publish(ts, round, (unsigned)s_pos[w],
-                       hit ? v3(s_o[w][0], s_o[w][1], s_o[w][2]) : v3(0.0f, 0.0f, 0.0f));
-        }
-        // every thread t < T collects slot t; block-wide minimum position
-        {
+        if (!resolve) {
+          // ---------------------------------------------------------------- SCAN
+          const int base = j + ((int)blockIdx.x * 4 + wave) * 64;
+          const int idx = base + lane;
+          const bool valid = idx < end;
+          V3 o = c;
+          if (valid) {
+            int zero = 0;
+            o = carry_path(sc, dep_rec[idx], maxrec, c, zero);
+          }
+          const unsigned long long m = __ballot(valid && !same_bits(o, c));
+          const int k = m ? __ffsll((long long)m) - 1 : -1;
+          if (lane == 0) s_pos[wave] = k >= 0 ? base + k : 0x7fffffff;
+          if (k >= 0 && lane == k) {
+            s_o[wave][0] = o.x;
+            s_o[wave][1] = o.y;
+            s_o[wave][2] = o.z;
+          }
+          __syncthreads();
+          if (threadIdx.x == 0) {
+            int w = 0;
+            for (int q = 1; q < 4; ++q)
+              if (s_pos[q] < s_pos[w]) w = q;
+            const bool hit = s_pos[w] != 0x7fffffff;
+            team_publish(ts, round, (unsigned)s_pos[w],
+                         hit ? v3(s_o[w][0], s_o[w][1], s_o[w][2]) : v3(0.0f, 0.0f, 0.0f));
+          }
+          // every thread t < T collects slot t; block-wide minimum position
           unsigned upos = 0x7fffffffu;
           V3 oc = v3(0.0f, 0.0f, 0.0f);
           bool ok = true;
@@ -610,22 +609,51 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
             s_nc[1] = oc.y;
             s_nc[2] = oc.z;
           }
-        }
-        __syncthreads();
-        const int gpos = s_gpos;
-        // entries before the first changer, and the changer itself, read carry c
-        if (valid && idx <= gpos) cin[idx] = make_float4(c.x, c.y, c.z, 0.0f);
-        if (gpos == 0x7fffffff) {
-          j += T * 4 * per_wave;
+          __syncthreads();
+          const int gpos = s_gpos;
+          // entries before the first changer, and the changer itself, read carry c
+          if (valid && idx <= gpos) cin[idx] = make_float4(c.x, c.y, c.z, 0.0f);
+          if (gpos == 0x7fffffff) {
+            j += window;
+          } else {
+            j = gpos + 1;
+            c = v3(s_nc[0], s_nc[1], s_nc[2]);
+            resolve = true;
+          }
+          __syncthreads();
         } else {
-          j = gpos + 1;
+          // ------------------------------------------------------------- RESOLVE
+          if (blockIdx.x == 0 && wave == 0) {
+            while (j < end) {
+              V3 mine;
+              const int evals = wave_window(sc, maxrec, dep_rec, j, end, c, mine, ls, G);
+              if (j + lane < end) cin[j + lane] = make_float4(mine.x, mine.y, mine.z, 0.0f);
+              j = j + 64 < end ? j + 64 : end;
+              if (evals == 1) break;   // a clean window: the cluster is over
+            }
+            if (lane == 0) team_publish(ts, round, (unsigned)j, c);
+          }
+          if (threadIdx.x == 0) {
+            unsigned upos = 0;
+            V3 oc;
+            const bool ok = team_collect(ts, round, 0, upos, oc);
+            s_gpos = ok ? (int)upos : -1;
+            s_nc[0] = oc.x;
+            s_nc[1] = oc.y;
+            s_nc[2] = oc.z;
+          }
+          __syncthreads();
+          if (s_gpos < 0) return;
+          j = s_gpos;
           c = v3(s_nc[0], s_nc[1], s_nc[2]);
+          resolve = false;
+          __syncthreads();
         }
-        __syncthreads();
       }
       if (trace && blockIdx.x == 0 && threadIdx.x == 0) {
-        trace[2 * s] = (unsigned)(__builtin_amdgcn_s_memrealtime() - t_seg);
-        trace[2 * s + 1] = (unsigned)rounds_here | 0x80000000u;
+        trace[3 * s] = (unsigned)(__builtin_amdgcn_s_memrealtime() - t_seg);
+        trace[3 * s + 1] = (unsigned)rounds_here | 0x80000000u;
+        trace[3 * s + 2] = (unsigned)(__builtin_amdgcn_s_memtime() - c_seg);
       }
     }
     return;
@@ -641,6 +669,7 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
     const int end = (s + 1 < nseg) ? seg_start[s + 1] : ndep;
     if (team_blocks > 0 && end - start >= long_len) continue;
     const unsigned long long t_seg = __builtin_amdgcn_s_memrealtime();
+    const unsigned long long c_seg = __builtin_amdgcn_s_memtime();
     int iters = 0;
     V3 c = seg_init_carry(dep_key, wcarry, start);
     for (int j = start; j < end; j += 64) {
@@ -649,8 +678,9 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
       if (j + lane < end) cin[j + lane] = make_float4(mine.x, mine.y, mine.z, 0.0f);
     }
     if (trace && lane == 0) {
-      trace[2 * s] = (unsigned)(__builtin_amdgcn_s_memrealtime() - t_seg);
-      trace[2 * s + 1] = (unsigned)iters;
+      trace[3 * s] = (unsigned)(__builtin_amdgcn_s_memrealtime() - t_seg);
+      trace[3 * s + 1] = (unsigned)iters;
+      trace[3 * s + 2] = (unsigned)(__builtin_amdgcn_s_memtime() - c_seg);
     }
   }
 }
