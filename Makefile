@@ -29,7 +29,7 @@ HIP_SRCS  := $(SRC)/rc_kernels.hip $(SRC)/rc_api.hip
 HIP_HDRS  := $(SRC)/rc_device.hpp $(SRC)/rc_kernels.h $(SRC)/rc_scene.h include/raycast_hip.h
 FRONT_SRC := $(SRC)/front/parse.c $(SRC)/front/objects.c $(SRC)/front/ppm.c
 
-.PHONY: all oracle ref clean
+.PHONY: all oracle ref clean stamps
 all: $(LIB)/libraycast_hip.so $(LIB)/libraycast_front.so $(BIN)/raytrace oracle
 
 $(OBJ)/%.o: $(SRC)/%.hip $(HIP_HDRS)
@@ -50,6 +50,17 @@ $(LIB)/libraycast_front.so: $(FRONT_SRC) include/raycast_hip.h
 $(BIN)/raytrace: $(SRC)/front/raytrace_main.c $(LIB)/libraycast_front.so $(LIB)/libraycast_hip.so
 	@mkdir -p $(BIN)
 	$(CC) $(CFLAGS) $< -L$(LIB) -lraycast_front -lraycast_hip -Wl,-rpath,'$$ORIGIN/../lib' -o $@
+
+# diagnostic build with in-kernel cycle stamps (RC_HIP_LIB=libraycast_hip_stamps.so)
+stamps: $(LIB)/libraycast_hip_stamps.so
+$(OBJ)/stamps_kernels.o: $(SRC)/rc_kernels.hip $(HIP_HDRS)
+	@mkdir -p $(OBJ)
+	$(HIPCC) $(HIPFLAGS) -DRC_STAMPS=1 -c $< -o $@
+$(OBJ)/stamps_api.o: $(SRC)/rc_api.hip $(HIP_HDRS)
+	@mkdir -p $(OBJ)
+	$(HIPCC) $(HIPFLAGS) -DRC_STAMPS=1 -c $< -o $@
+$(LIB)/libraycast_hip_stamps.so: $(OBJ)/stamps_kernels.o $(OBJ)/stamps_api.o $(OBJ)/rc_scene.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -o $@ -lpthread
 
 oracle:
 	$(MAKE) -C oracle oracle

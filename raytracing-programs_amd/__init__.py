@@ -105,7 +105,8 @@ def front_lib():
 
 
 def hip_lib():
-    lib = _load("libraycast_hip.so")
+    # RC_HIP_LIB selects a diagnostic build (e.g. libraycast_hip_stamps.so); never the default
+    lib = _load(os.environ.get("RC_HIP_LIB", "libraycast_hip.so"))
     lib.rc_scene_create.argtypes = [ctypes.POINTER(JsonDataT)]
     lib.rc_scene_create.restype = ctypes.c_void_p
     lib.rc_scene_destroy.argtypes = [ctypes.c_void_p]

@@ -176,6 +176,10 @@ int upload_scene(DevCtx& c, const rc_scene* s, rc::LaunchScene& ls) {
   ls.m = h->m;
   ls.cam_w = h->cam_w;
   ls.cam_h = h->cam_h;
+  ls.refl_mask = 0;
+  const rc_shape* hs = (const rc_shape*)((const char*)h + h->off_shapes);
+  for (int k = 0; k < h->n && k < 64; ++k)
+    if (hs[k].refl > 0.0f) ls.refl_mask |= 1ull << k;
   return 0;
 }
 
@@ -234,7 +238,7 @@ int ensure_parity(DevCtx& c, int W, int H, rc::ParityWork& w) {
   }
   w.trace = nullptr;
   if (std::getenv("RC_RESOLVE_TRACE")) {
-    if (c.trace.ensure(P * 3 * sizeof(unsigned))) return -1;
+    if (c.trace.ensure(P * 7 * sizeof(unsigned))) return -1;
     w.trace = (unsigned*)c.trace.p;
   }
   w.phase_c_blocks = c.cus * 8;
@@ -312,6 +316,19 @@ void fill_device_timing(DevCtx& c, const rc_options* opt, rc_timing* t) {
         }
         std::fclose(f);
       }
+#if RC_STAMPS
+      std::vector<unsigned> sp(4 * (size_t)cnt[0]);
+      (void)hipMemcpy(sp.data(), (const unsigned*)c.trace.p + 3 * (size_t)cnt[2],
+                      sp.size() * sizeof(unsigned), hipMemcpyDeviceToHost);
+      std::string p2 = std::string(path) + ".stamps";
+      if (FILE* f = std::fopen(p2.c_str(), "w")) {
+        for (int k = 0; k < cnt[0]; ++k)
+          if (sp[4 * k] | sp[4 * k + 1])
+            std::fprintf(f, "%d norm %u test %u argmin %u hit+loop %u\n", k, sp[4 * k],
+                         sp[4 * k + 1], sp[4 * k + 2], sp[4 * k + 3]);
+        std::fclose(f);
+      }
+#endif
     }
   }
 }

@@ -36,7 +36,14 @@ struct Scene {
   const rc_light* __restrict__ lights;   // m records
   const rc_shade_pair* __restrict__ pairs;
   int n, m;
+  unsigned long long refl_mask;          // bit k: shape k has reflectivity > 0 (k < 64)
 };
+
+// refl[obj] > 0 (C/raycast.c:352) from a register bitmask when n <= 64
+__device__ __forceinline__ bool reflective(const Scene& sc, int obj) {
+  if (sc.n <= 64) return (sc.refl_mask >> obj) & 1ull;
+  return sc.shapes[obj].refl > 0.0f;
+}
 
 struct Cam {
   double hx, hy;   // (0.0 - cw/2.0) and (0.0 + ch/2.0)      C/raycast.c:115-116
@@ -66,7 +73,9 @@ __device__ __forceinline__ float length(V3 a) {
 }
 
 // C/v3math.c:180-192 — a zero length leaves the vector unchanged (and is counted: the
-// reference prints a stderr line per event)
+// reference prints a stderr line per event).  (A shared-reciprocal variant — provably exact
+// for float quotients, q = RN32((double)a * r) — was measured slower on gfx950: v_rcp_f64 and
+// the extra f64 ops cost more latency than three full-rate IEEE f32 divisions.)
 __device__ __forceinline__ V3 normalize(V3 a, int& zero_events) {
   float len = length(a);
   if (len == 0.0f) {
@@ -471,15 +480,38 @@ struct LaneShape {
   bool has;
 };
 
-__device__ __forceinline__ int group_argmin(float& t, int k, int G) {
-  for (int off = 1; off < G; off <<= 1) {
-    const float t2 = __shfl_xor(t, off, 64);
-    const int k2 = __shfl_xor(k, off, 64);
-    if (t2 < t || (t2 == t && k2 < k)) {
-      t = t2;
-      k = k2;
-    }
+// Cross-lane moves inside 16-lane rows use DPP (a VALU modifier, a few cycles) instead of
+// ds_bpermute (an LDS round trip, ~50 cycles): this argmin sits on the serial chain.
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int v) {
+  return __builtin_amdgcn_update_dpp(v, v, CTRL, 0xF, 0xF, false);
+}
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), CTRL,
+                                                    0xF, 0xF, false));
+}
+constexpr int kDppXor1 = 0xB1;        // quad_perm [1,0,3,2]
+constexpr int kDppXor2 = 0x4E;        // quad_perm [2,3,0,1]
+constexpr int kDppHalfMirror = 0x141; // row_half_mirror: lane i <-> 7-i within 8 lanes
+constexpr int kDppRor8 = 0x128;       // row_ror:8: the other 8-lane half of a 16-lane row
+
+__device__ __forceinline__ void argmin_step(float& t, int& k, float t2, int k2) {
+  if (t2 < t || (t2 == t && k2 < k)) {
+    t = t2;
+    k = k2;
   }
+}
+
+__device__ __forceinline__ int group_argmin(float& t, int k, int G) {
+  if (G >= 2) argmin_step(t, k, dpp_f<kDppXor1>(t), dpp_i<kDppXor1>(k));
+  if (G >= 4) argmin_step(t, k, dpp_f<kDppXor2>(t), dpp_i<kDppXor2>(k));
+  // after the quad steps every lane of a quad holds the quad minimum, so mirroring the
+  // 8-lane half pairs quad 0 with quad 1
+  if (G >= 8) argmin_step(t, k, dpp_f<kDppHalfMirror>(t), dpp_i<kDppHalfMirror>(k));
+  if (G >= 16) argmin_step(t, k, dpp_f<kDppRor8>(t), dpp_i<kDppRor8>(k));
+  for (int off = 16; off < G; off <<= 1)
+    argmin_step(t, k, __shfl_xor(t, off, 64), __shfl_xor(k, off, 64));
   return k;
 }
 
@@ -490,7 +522,7 @@ __device__ __forceinline__ V3 carry_path_coop(const Scene& sc, const LaneShape& 
   V3 D = v3(r.d1x, r.d1y, r.d1z), N = v3(r.n0x, r.n0y, r.n0z), C = c;
   int obj = r.obj0, S = -1;
   for (int lvl = 2; lvl < maxrec; ++lvl) {
-    if (!(sc.shapes[obj].refl > 0.0f)) break;
+    if (!reflective(sc, obj)) break;
     D = normalize(reflect(D, N), zero_events);
     const RayK rk = ray_consts(D);
     float t = __builtin_inff();
@@ -520,6 +552,34 @@ __device__ __forceinline__ V3 carry_path_coop(const Scene& sc, const LaneShape& 
 
 namespace rc {
 
+// Diagnostic build only (-DRC_STAMPS=1, `make stamps`): per-section cycle sums of the
+// speculative evaluator, read by the resolver trace.  The shipped library has no stamps.
+#if RC_STAMPS
+struct Stamps {
+  unsigned long long acc[4];
+  unsigned long long last;
+};
+__device__ __forceinline__ unsigned long long stamp_now() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+#define RC_STAMP_DECL Stamps* st_
+#define RC_STAMP_ARG , st_
+#define RC_STAMP(i)                                  \
+  do {                                               \
+    const unsigned long long n_ = stamp_now();       \
+    st_->acc[i] += n_ - st_->last;                   \
+    st_->last = n_;                                  \
+  } while (0)
+#else
+#define RC_STAMP(i) \
+  do {              \
+  } while (0)
+#endif
+
 // Cooperative evaluation with level speculation: the 2G lanes of one entry form two
 // groups.  Group h=0 evaluates bounce level L; group h=1 evaluates level L+1 assuming level
 // L misses — then its ray is fully known in advance: same origin C, direction
@@ -529,7 +589,11 @@ namespace rc {
 // five levels retire in three steps.
 __device__ __forceinline__ V3 carry_path_spec(const Scene& sc, const LaneShape& ls, int kself,
                                               int G, int half, const DepRec& r, int maxrec,
-                                              V3 c, int& zero_events) {
+                                              V3 c, int& zero_events
+#if RC_STAMPS
+                                              , Stamps* st_
+#endif
+) {
   constexpr int kNone = 0x7fffffff;
   V3 D = v3(r.d1x, r.d1y, r.d1z), N = v3(r.n0x, r.n0y, r.n0z), C = c;
   int obj = r.obj0, S = -1;
@@ -538,9 +602,11 @@ __device__ __forceinline__ V3 carry_path_spec(const Scene& sc, const LaneShape& 
   const int lead1 = lead0 + G;             // group h=1 leader
   int lvl = 2;
   while (lvl < maxrec) {
-    if (!(sc.shapes[obj].refl > 0.0f)) break;
+    if (!reflective(sc, obj)) break;
+    RC_STAMP(3);
     const V3 D1 = normalize(reflect(D, N), zero_events);
     const V3 D2 = normalize(reflect(D1, N), zero_events);
+    RC_STAMP(0);
     const V3 myD = half ? D2 : D1;
     const int myS = half ? -1 : S;
     const RayK rk = ray_consts(myD);
@@ -553,9 +619,20 @@ __device__ __forceinline__ V3 carry_path_spec(const Scene& sc, const LaneShape& 
         k = kself;
       }
     }
+    RC_STAMP(1);
     k = group_argmin(t, k, G);
-    const int w0 = __shfl(k, lead0, 64), w1 = __shfl(k, lead1, 64);
-    const float t0 = __shfl(t, lead0, 64), t1 = __shfl(t, lead1, 64);
+    int ko;
+    float to;
+    if (G == 8) {          // the two halves are the 8-lane halves of one 16-lane row
+      ko = dpp_i<kDppRor8>(k);
+      to = dpp_f<kDppRor8>(t);
+    } else {
+      ko = __shfl(k, half ? lead0 : lead1, 64);
+      to = __shfl(t, half ? lead0 : lead1, 64);
+    }
+    const int w0 = half ? ko : k, w1 = half ? k : ko;
+    const float t0 = half ? to : t, t1 = half ? t : to;
+    RC_STAMP(2);
     if (w0 != kNone) {                       // level L hits
       V3 P;
       hit_frame(sc, w0, C, D1, t0, P, N, zero_events);

@@ -16,6 +16,7 @@ struct LaunchScene {
   const rc_shade_pair* pairs;
   int n, m;
   float cam_w, cam_h;
+  unsigned long long refl_mask;   // bit k: shape k reflective (n <= 64)
 };
 
 // Parity-mode workspace (device pointers), sized for W*H pixels.

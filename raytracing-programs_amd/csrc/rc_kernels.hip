@@ -377,10 +377,20 @@ __device__ __forceinline__ DepRec shfl_rec(const DepRec& r, int src) {
   return o;
 }
 
+// Window state machine.  LANE: one entry per lane at the current carry (64 entries for one
+// evaluation's latency: right for clean stretches).  COOP: the cooperative evaluator, 64/GE
+// entries per step at a lower latency (right inside dense runs, where every entry may move
+// the carry).  A changer found by a LANE pass switches to COOP; two clean COOP steps in a row
+// switch back.  `dense` carries the mode into the next window.  Returns the number of
+// evaluation steps; *changed tells whether any entry of the window moved the carry.
 __device__ __forceinline__ int wave_window(const Scene& sc, int maxrec,
                                            const DepRec* __restrict__ dep_rec, int base,
                                            int end, V3& c, V3& mine, const LaneShape& ls,
-                                           int G) {
+                                           int G, bool& dense, bool& changed
+#if RC_STAMPS
+                                           , Stamps* st_
+#endif
+) {
   const int lane = threadIdx.x & 63;
   const int idx = base + lane;
   const int nvalid = end - base < 64 ? end - base : 64;
@@ -388,59 +398,64 @@ __device__ __forceinline__ int wave_window(const Scene& sc, int maxrec,
   DepRec r;
   if (valid) r = dep_rec[idx];
   mine = c;
+  changed = false;
   int zero = 0;
-  V3 o = c;
-  if (valid) o = carry_path(sc, r, maxrec, c, zero);
-  unsigned long long m = __ballot(valid && !same_bits(o, c));
-  int evals = 1;
-  if (m == 0) return evals;
-  int k = __ffsll((long long)m) - 1;
-  c = v3(__shfl(o.x, k, 64), __shfl(o.y, k, 64), __shfl(o.z, k, 64));
-  int pos = k + 1;   // lanes < pos resolved (their mine is the carry they were read with)
-  if (G > 0) {
-    // speculative pairs when two groups fit per entry, else one group per entry
-    const bool spec = 2 * G <= 64;
-    const int GE = spec ? 2 * G : G;          // lanes per entry
-    const int E = 64 / GE;
-    const int e = lane / GE, kself = lane % G, half = spec ? (lane / G) & 1 : 0;
-    while (pos < nvalid) {
-      ++evals;
-      const int i = pos + e;
-      const bool act = e < E && i < nvalid;
-      const DepRec ri = shfl_rec(r, i < 64 ? i : 63);
-      V3 oc = c;
-      if (act)
-        oc = spec ? carry_path_spec(sc, ls, kself, G, half, ri, maxrec, c, zero)
-                  : carry_path_coop(sc, ls, kself, G, ri, maxrec, c, zero);
-      const unsigned long long mc = __ballot(act && (lane % GE) == 0 && !same_bits(oc, c));
-      if (mc == 0) {
-        const int lim = pos + E < nvalid ? pos + E : nvalid;
-        if (lane >= pos && lane < lim) mine = c;
-        pos = lim;
-        continue;
-      }
-      const int g = (__ffsll((long long)mc) - 1) / GE;
-      if (lane >= pos && lane <= pos + g) mine = c;
-      c = v3(__shfl(oc.x, g * GE, 64), __shfl(oc.y, g * GE, 64), __shfl(oc.z, g * GE, 64));
-      pos += g + 1;
-    }
-    return evals;
-  }
-  // no cooperative evaluator (more than 64 shapes): per-lane steps
-  bool active = valid && lane >= pos;
-  while (__ballot(active)) {
+  int evals = 0;
+  int pos = 0;                     // lanes < pos are resolved
+  bool coop = dense && G > 0;
+  int clean_run = 0;
+  const bool spec = 2 * G <= 64;
+  const int GE = G > 0 ? (spec ? 2 * G : G) : 64;
+  const int E = 64 / GE;
+  const int e = lane / GE, kself = G > 0 ? lane % G : 0, half = spec ? (lane / G) & 1 : 0;
+  while (pos < nvalid) {
     ++evals;
-    if (active) o = carry_path(sc, r, maxrec, c, zero);
-    m = __ballot(active && !same_bits(o, c));
-    if (m == 0) {
-      if (active) mine = c;
-      break;
+    if (!coop) {
+      const bool act = valid && lane >= pos;
+      V3 o = c;
+      if (act) o = carry_path(sc, r, maxrec, c, zero);
+      const unsigned long long m = __ballot(act && !same_bits(o, c));
+      if (m == 0) {
+        if (act) mine = c;
+        pos = nvalid;
+        break;
+      }
+      const int k = __ffsll((long long)m) - 1;
+      if (act && lane <= k) mine = c;
+      c = v3(__shfl(o.x, k, 64), __shfl(o.y, k, 64), __shfl(o.z, k, 64));
+      pos = k + 1;
+      changed = true;
+      coop = G > 0;
+      clean_run = 0;
+      continue;
     }
-    k = __ffsll((long long)m) - 1;
-    if (active && lane <= k) mine = c;
-    c = v3(__shfl(o.x, k, 64), __shfl(o.y, k, 64), __shfl(o.z, k, 64));
-    active = active && lane > k;
+    const int i = pos + e;
+    const bool act = e < E && i < nvalid;
+    const DepRec ri = shfl_rec(r, i < 64 ? i : 63);
+    V3 oc = c;
+    if (act)
+      oc = spec ? carry_path_spec(sc, ls, kself, G, half, ri, maxrec, c, zero
+#if RC_STAMPS
+                                  , st_
+#endif
+                                  )
+                : carry_path_coop(sc, ls, kself, G, ri, maxrec, c, zero);
+    const unsigned long long mc = __ballot(act && (lane % GE) == 0 && !same_bits(oc, c));
+    if (mc == 0) {
+      const int lim = pos + E < nvalid ? pos + E : nvalid;
+      if (lane >= pos && lane < lim) mine = c;
+      pos = lim;
+      if (++clean_run >= 2) coop = false;
+      continue;
+    }
+    const int g = (__ffsll((long long)mc) - 1) / GE;
+    if (lane >= pos && lane <= pos + g) mine = c;
+    c = v3(__shfl(oc.x, g * GE, 64), __shfl(oc.y, g * GE, 64), __shfl(oc.z, g * GE, 64));
+    pos += g + 1;
+    changed = true;
+    clean_run = 0;
   }
+  dense = coop;
   return evals;
 }
 
@@ -521,6 +536,9 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
     __syncthreads();
     sc.shapes = s_shapes;
   }
+#if RC_STAMPS
+  Stamps stp = {{0, 0, 0, 0}, 0};
+#endif
   LaneShape ls;
   ls.has = false;
   if (G > 0) {
@@ -624,12 +642,18 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
         } else {
           // ------------------------------------------------------------- RESOLVE
           if (blockIdx.x == 0 && wave == 0) {
+            bool dense = true;   // the cluster starts right after a changer
             while (j < end) {
               V3 mine;
-              const int evals = wave_window(sc, maxrec, dep_rec, j, end, c, mine, ls, G);
+              bool changed;
+              wave_window(sc, maxrec, dep_rec, j, end, c, mine, ls, G, dense, changed
+#if RC_STAMPS
+                          , &stp
+#endif
+                          );
               if (j + lane < end) cin[j + lane] = make_float4(mine.x, mine.y, mine.z, 0.0f);
               j = j + 64 < end ? j + 64 : end;
-              if (evals == 1) break;   // a clean window: the cluster is over
+              if (!changed) break;   // a clean window: the cluster is over
             }
             if (lane == 0) team_publish(ts, round, (unsigned)j, c);
           }
@@ -672,11 +696,23 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
     const unsigned long long c_seg = __builtin_amdgcn_s_memtime();
     int iters = 0;
     V3 c = seg_init_carry(dep_key, wcarry, start);
+    bool dense = false;
     for (int j = start; j < end; j += 64) {
       V3 mine;
-      iters += wave_window(sc, maxrec, dep_rec, j, end, c, mine, ls, G);
+      bool changed;
+      iters += wave_window(sc, maxrec, dep_rec, j, end, c, mine, ls, G, dense, changed
+#if RC_STAMPS
+                           , &stp
+#endif
+                           );
       if (j + lane < end) cin[j + lane] = make_float4(mine.x, mine.y, mine.z, 0.0f);
     }
+#if RC_STAMPS
+    if (trace && lane == 0 && end - start > 1000) {
+      for (int q = 0; q < 4; ++q) trace[3 * ndep + 4 * s + q] = (unsigned)stp.acc[q];
+    }
+    for (int q = 0; q < 4; ++q) stp.acc[q] = 0;
+#endif
     if (trace && lane == 0) {
       trace[3 * s] = (unsigned)(__builtin_amdgcn_s_memrealtime() - t_seg);
       trace[3 * s + 1] = (unsigned)iters;
@@ -714,6 +750,7 @@ static Scene make_scene(const LaunchScene& s) {
   sc.pairs = s.pairs;
   sc.n = s.n;
   sc.m = s.m;
+  sc.refl_mask = s.refl_mask;
   return sc;
 }
 static Cam make_cam(const LaunchScene& s, int W, int H) {
