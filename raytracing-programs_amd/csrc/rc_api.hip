@@ -232,7 +232,7 @@ int ensure_parity(DevCtx& c, int W, int H, rc::ParityWork& w) {
   w.coop_group = 0;
   if (!std::getenv("RC_NO_COOP") && c.scene_src) {
     const int n = ((const rc_packed_header*)c.scene_src)->n;
-    int g = 1;
+    int g = 4;   // groups of >= 4 lanes: the evaluator is specialised for 4, 8 and 16
     while (g < n) g <<= 1;
     if (n >= 1 && g <= 64) w.coop_group = g;
   }

@@ -515,6 +515,34 @@ __device__ __forceinline__ int group_argmin(float& t, int k, int G) {
   return k;
 }
 
+// Branch-free form for candidates with t in (0, +inf] (misses carry t = +inf, k = kNone):
+// positive floats order like their bit patterns, so the lexicographic (t, k) minimum is a
+// u32 min over t's bits, then a u32 min over k among the lanes holding that t.  Each step is
+// one DPP-fed v_min_u32 — no compare/select chains or exec-mask branches on the serial path.
+template <int CTRL>
+__device__ __forceinline__ unsigned dpp_min_u(unsigned v) {
+  return __builtin_elementwise_min(v, (unsigned)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF,
+                                                                         false));
+}
+template <int GT>
+__device__ __forceinline__ unsigned group_min_u(unsigned v, int Grt) {
+  const int G = GT ? GT : Grt;
+  if (G >= 2) v = dpp_min_u<kDppXor1>(v);
+  if (G >= 4) v = dpp_min_u<kDppXor2>(v);
+  if (G >= 8) v = dpp_min_u<kDppHalfMirror>(v);
+  if (G >= 16) v = dpp_min_u<kDppRor8>(v);
+  for (int off = 16; off < G; off <<= 1)
+    v = __builtin_elementwise_min(v, (unsigned)__shfl_xor((int)v, off, 64));
+  return v;
+}
+template <int GT>
+__device__ __forceinline__ int group_argmin_pos(float& t, int k, int G) {
+  const unsigned tb = group_min_u<GT>(__float_as_uint(t), G);
+  const unsigned kb = group_min_u<GT>(__float_as_uint(t) == tb ? (unsigned)k : 0xffffffffu, G);
+  t = __uint_as_float(tb);
+  return (int)kb;
+}
+
 __device__ __forceinline__ V3 carry_path_coop(const Scene& sc, const LaneShape& ls, int kself,
                                               int G, const DepRec& r, int maxrec, V3 c,
                                               int& zero_events) {
@@ -580,20 +608,153 @@ __device__ __forceinline__ unsigned long long stamp_now() {
   } while (0)
 #endif
 
+// ------------------------------------------------------ branch-free lane evaluation --
+// The cooperative groups hold one shape per lane, so a wave holds every shape type at once
+// and type-divergent code runs each type's branch (each with its own sqrt and divisions)
+// one after the other, with nothing to overlap on a lone wave.  The forms below compute
+// every type's prelude in straight-line code and share ONE f64 sqrt and two parallel f64
+// divisions, selecting by type at the end; each value is produced by the same operations in
+// the same order as hit_sphere / hit_plane / hit_quadric, so results are bit-identical.
+// The plane's f32 quotient (-num)/den is taken as (float)((double)(-num) / (double)den):
+// double rounding is innocuous for division when 53 >= 2*24 + 2.
+
+// normalize() without the branch (the zero-length case keeps the input, not counted: only
+// the final shading pass counts events).
+// Materialise a value in a register as an opaque definition.  Codegen otherwise turns a
+// select whose operand is an expensive single-use op (f64 division, sqrt) into a branch that
+// computes the operand conditionally, which serialises the independent quotients.
+template <class T>
+__device__ __forceinline__ T pin(T x) {
+  asm("" : "+v"(x));
+  return x;
+}
+
+// component-wise select (a struct-valued ?: becomes a pointer select over stack copies)
+__device__ __forceinline__ V3 sel(bool p, V3 a, V3 b) {
+  return v3(p ? a.x : b.x, p ? a.y : b.y, p ? a.z : b.z);
+}
+
+__device__ __forceinline__ V3 normalize_sel(V3 a) {
+  const float len = length(a);
+  return sel(len == 0.0f, a, v3(pin(a.x / len), pin(a.y / len), pin(a.z / len)));
+}
+
+// test_shape() for any type, branch-free.
+__device__ __forceinline__ bool test_unified(const rc_shape& s, V3 O, V3 D, RayK rk, int skip,
+                                             float& t) {
+  const int type = s.type;
+  const bool isS = type == RC_SHAPE_SPHERE, isP = type == RC_SHAPE_PLANE,
+             isQ = type == RC_SHAPE_QUADRIC;
+  // origin-only parts (sphere c, plane num, quadric cq)
+  const V3 tv = v3(O.x - s.p[0], O.y - s.p[1], O.z - s.p[2]);
+  const float cS = (float)((double)dot(tv, tv) - s.r2);
+  const float numP = pin(dot(tv, v3(s.n[0], s.n[1], s.n[2])));
+  double acc;
+  acc = s.A * ((double)O.x * (double)O.x);
+  acc = acc + s.B * ((double)O.y * (double)O.y);
+  acc = acc + s.C * ((double)O.z * (double)O.z);
+  acc = acc + (double)(s.qd * O.x * O.y);
+  acc = acc + (double)(s.qe * O.x * O.z);
+  acc = acc + (double)(s.qf * O.y * O.z);
+  acc = acc + (double)(s.qg * O.x);
+  acc = acc + (double)(s.qh * O.y);
+  acc = acc + (double)(s.qi * O.z);
+  acc = acc + (double)s.qj;
+  const float cq = (float)acc;
+  // direction parts
+  const float bS = 2.0f * dot(D, tv);
+  const float facS = rk.a4 * cS;
+  const float discS = (float)((double)bS * (double)bS - (double)facS);
+  const float denP = dot(D, v3(s.n[0], s.n[1], s.n[2]));
+  acc = s.A * ((double)D.x * (double)D.x);
+  acc = acc + s.B * ((double)D.y * (double)D.y);
+  acc = acc + s.C * ((double)D.z * (double)D.z);
+  acc = acc + (double)(s.qd * D.x * D.y);
+  acc = acc + (double)(s.qe * D.x * D.z);
+  acc = acc + (double)(s.qf * D.y * D.z);
+  const float aq = (float)acc;
+  acc = 2.0 * s.A * (double)O.x * (double)D.x;
+  acc = acc + 2.0 * s.B * (double)O.y * (double)D.y;
+  acc = acc + 2.0 * s.C * (double)O.z * (double)D.z;
+  acc = acc + (double)(s.qd * (O.x * D.y + O.y * D.x));
+  acc = acc + (double)(s.qe * (O.x * D.z + O.z * D.x));
+  acc = acc + (double)(s.qf * (O.y * D.z + O.z * D.y));
+  acc = acc + (double)(s.qg * D.x);
+  acc = acc + (double)(s.qh * D.y);
+  acc = acc + (double)(s.qi * D.z);
+  const float bq = (float)acc;
+  const float discQ = (float)((double)bq * (double)bq - 4.0 * (double)aq * (double)cq);
+  const bool lin = (double)aq == 0.0;
+  // shared tail: one sqrt, two quotients
+  const float B = isS ? bS : bq;
+  const float disc = isS ? discS : discQ;
+  const double sq = pin(__builtin_sqrt((double)disc));
+  const double nb = (double)(-B);
+  const bool qlin = isQ & lin;
+  const double n1q = pin(nb - sq), n1l = pin(-1.0 * (double)cq), n1p = pin((double)(-numP));
+  const double num1 = isP ? n1p : (qlin ? n1l : n1q);
+  const double den1 = isP ? (double)denP : (qlin ? (double)bq : (isS ? rk.den : 2.0 * (double)aq));
+  const double num2 = nb + sq;
+  const float q1 = (float)pin(num1 / den1);
+  const float q2 = (float)pin(num2 / den1);
+  // sphere: second root if the first is negative; quadric: if it is not positive
+  const bool second = (isS & (q1 < 0.0f)) | (isQ & !lin & (q1 <= 0.0f));
+  const float tt = second ? q2 : q1;
+  const bool okS = isS & !(disc < 0.0f);
+  const bool okP = isP & (denP != 0.0f) & !(q1 < 0.0f);
+  const bool okQ = isQ & (lin | !((double)disc < 0.0));
+  // C/raycast.c:492-494: a bounce ray ignores quadric hits below its origin's z
+  const bool below = isQ & (skip != -1) & ((O.z + tt * D.z) < O.z);
+  const bool ok = (okS | okP | okQ) & !below;
+  t = tt;
+  return ok;
+}
+
+// hit_frame() without type branches; `s` is the winner's record.
+__device__ __forceinline__ void hit_frame_sel(const rc_shape& s, V3 O, V3 D, float t, V3& P,
+                                              V3& N) {
+  P = v3(O.x + D.x * t, O.y + D.y * t, O.z + D.z * t);
+  const int type = s.type;
+  const float inv = s.inv_r;
+  const V3 vs = v3((P.x - s.p[0]) * inv, (P.y - s.p[1]) * inv, (P.z - s.p[2]) * inv);
+  double n0 = 2.0 * s.A * (double)P.x;
+  n0 = n0 + (double)(s.qd * P.y);
+  n0 = n0 + (double)(s.qe * P.z);
+  n0 = n0 + (double)s.qg;
+  double n1 = 2.0 * s.B * (double)P.y;
+  n1 = n1 + (double)(s.qd * P.x);
+  n1 = n1 + (double)(s.qf * P.z);
+  n1 = n1 + (double)s.qh;
+  double n2 = 2.0 * s.C * (double)P.z;
+  n2 = n2 + (double)(s.qe * P.x);
+  n2 = n2 + (double)(s.qf * P.y);
+  n2 = n2 + (double)s.qi;
+  const bool isS = type == RC_SHAPE_SPHERE, isP = type == RC_SHAPE_PLANE;
+  const V3 v = sel(isS, vs, v3((float)n0, (float)n1, (float)n2));
+  V3 n = normalize_sel(v);
+  n = sel(!isS && dot(n, D) > 0.0f, v3(n.x * -1.0f, n.y * -1.0f, n.z * -1.0f), n);
+  N = sel(isP, v3(s.n[0], s.n[1], s.n[2]), n);
+}
+
 // Cooperative evaluation with level speculation: the 2G lanes of one entry form two
 // groups.  Group h=0 evaluates bounce level L; group h=1 evaluates level L+1 assuming level
 // L misses — then its ray is fully known in advance: same origin C, direction
 // normalize(reflect(D_L, N)), skip -1, and the object test refl[obj] > 0 unchanged
 // (C/raycast.c:349-367 with the stale object/normal of a miss).  If level L misses, both
 // levels retire in one step.  The carry creep of dense segments alternates hit/miss, so
-// five levels retire in three steps.
+// five levels retire in three steps.  Each step is one basic block (selects, no branches)
+// so the scheduler can overlap the independent chains of a lone wave.  GT = the group size
+// as a compile-time constant (4, 8, 16), or 0 for the runtime value Grt.
+template <int GT>
 __device__ __forceinline__ V3 carry_path_spec(const Scene& sc, const LaneShape& ls, int kself,
-                                              int G, int half, const DepRec& r, int maxrec,
+                                              int Grt, int half, const DepRec& r, int maxrec,
                                               V3 c, int& zero_events
 #if RC_STAMPS
                                               , Stamps* st_
 #endif
 ) {
+  (void)zero_events;
+  const int G = GT ? GT : Grt;
   constexpr int kNone = 0x7fffffff;
   V3 D = v3(r.d1x, r.d1y, r.d1z), N = v3(r.n0x, r.n0y, r.n0z), C = c;
   int obj = r.obj0, S = -1;
@@ -604,28 +765,27 @@ __device__ __forceinline__ V3 carry_path_spec(const Scene& sc, const LaneShape& 
   while (lvl < maxrec) {
     if (!reflective(sc, obj)) break;
     RC_STAMP(3);
-    const V3 D1 = normalize(reflect(D, N), zero_events);
-    const V3 D2 = normalize(reflect(D1, N), zero_events);
+    const V3 D1 = normalize_sel(reflect(D, N));
+    const V3 D2 = normalize_sel(reflect(D1, N));
     RC_STAMP(0);
-    const V3 myD = half ? D2 : D1;
+    const V3 myD = sel(half, D2, D1);
     const int myS = half ? -1 : S;
     const RayK rk = ray_consts(myD);
-    float t = __builtin_inff();
-    int k = kNone;
-    if (ls.has && kself != myS) {
-      float tt = 0.0f;
-      if (test_shape(ls.s, C, myD, rk, myS, tt) && __builtin_inff() > tt && tt > 0.0f) {
-        t = tt;
-        k = kself;
-      }
-    }
+    float tt = 0.0f;
+    const bool ok = test_unified(ls.s, C, myD, rk, myS, tt) && ls.has && kself != myS &&
+                    __builtin_inff() > tt && tt > 0.0f;
+    float t = ok ? tt : __builtin_inff();
+    int k = ok ? kself : kNone;
     RC_STAMP(1);
-    k = group_argmin(t, k, G);
+    k = group_argmin_pos<GT>(t, k, G);
     int ko;
     float to;
-    if (G == 8) {          // the two halves are the 8-lane halves of one 16-lane row
+    if (GT == 8) {          // the two halves are the 8-lane halves of one 16-lane row
       ko = dpp_i<kDppRor8>(k);
       to = dpp_f<kDppRor8>(t);
+    } else if (GT == 4) {   // the two quads of an 8-lane half (each quad holds its minimum)
+      ko = dpp_i<kDppHalfMirror>(k);
+      to = dpp_f<kDppHalfMirror>(t);
     } else {
       ko = __shfl(k, half ? lead0 : lead1, 64);
       to = __shfl(t, half ? lead0 : lead1, 64);
@@ -633,31 +793,21 @@ __device__ __forceinline__ V3 carry_path_spec(const Scene& sc, const LaneShape& 
     const int w0 = half ? ko : k, w1 = half ? k : ko;
     const float t0 = half ? to : t, t1 = half ? t : to;
     RC_STAMP(2);
-    if (w0 != kNone) {                       // level L hits
-      V3 P;
-      hit_frame(sc, w0, C, D1, t0, P, N, zero_events);
-      C = P;
-      obj = w0;
-      S = w0;
-      D = D1;
-      lvl += 1;
-    } else if (lvl + 1 < maxrec) {           // level L misses: level L+1 was speculated
-      if (w1 != kNone) {
-        V3 P;
-        hit_frame(sc, w1, C, D2, t1, P, N, zero_events);
-        C = P;
-        obj = w1;
-        S = w1;
-      } else {
-        S = -1;
-      }
-      D = D2;
-      lvl += 2;
-    } else {
-      S = -1;
-      D = D1;
-      lvl += 1;
-    }
+    // level L hits: retire L.  Level L misses and L+1 exists: retire both (L+1 may miss).
+    const bool hitL = w0 != kNone;
+    const bool two = !hitL && lvl + 1 < maxrec;
+    const int w = hitL ? w0 : (two ? w1 : kNone);
+    const float tw = hitL ? t0 : t1;
+    const V3 Dw = sel(two, D2, D1);
+    const bool hit = w != kNone;
+    V3 P, Nw;
+    hit_frame_sel(sc.shapes[hit ? w : 0], C, Dw, tw, P, Nw);
+    C = sel(hit, P, C);
+    N = sel(hit, Nw, N);
+    obj = hit ? w : obj;
+    S = hit ? w : -1;
+    D = Dw;
+    lvl += two ? 2 : 1;
   }
   return C;
 }

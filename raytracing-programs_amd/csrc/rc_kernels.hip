@@ -433,13 +433,19 @@ __device__ __forceinline__ int wave_window(const Scene& sc, int maxrec,
     const bool act = e < E && i < nvalid;
     const DepRec ri = shfl_rec(r, i < 64 ? i : 63);
     V3 oc = c;
-    if (act)
-      oc = spec ? carry_path_spec(sc, ls, kself, G, half, ri, maxrec, c, zero
 #if RC_STAMPS
-                                  , st_
+#define RC_SPEC(GT) carry_path_spec<GT>(sc, ls, kself, G, half, ri, maxrec, c, zero, st_)
+#else
+#define RC_SPEC(GT) carry_path_spec<GT>(sc, ls, kself, G, half, ri, maxrec, c, zero)
 #endif
-                                  )
-                : carry_path_coop(sc, ls, kself, G, ri, maxrec, c, zero);
+    if (act) {
+      if (G == 8) oc = RC_SPEC(8);
+      else if (G == 4) oc = RC_SPEC(4);
+      else if (G == 16) oc = RC_SPEC(16);
+      else if (spec) oc = RC_SPEC(0);
+      else oc = carry_path_coop(sc, ls, kself, G, ri, maxrec, c, zero);
+    }
+#undef RC_SPEC
     const unsigned long long mc = __ballot(act && (lane % GE) == 0 && !same_bits(oc, c));
     if (mc == 0) {
       const int lim = pos + E < nvalid ? pos + E : nvalid;
