@@ -353,6 +353,11 @@ static void o_build_phantom(octx *c) {
 
 int rco_render(const json_data_t *js, int width, int height, int max_recursion, int mode,
                uint8_t *pixmap, rco_stats *stats, float *carry_in) {
+  return rco_render_cls(js, width, height, max_recursion, mode, pixmap, stats, carry_in, NULL);
+}
+
+int rco_render_cls(const json_data_t *js, int width, int height, int max_recursion, int mode,
+                   uint8_t *pixmap, rco_stats *stats, float *carry_in, uint8_t *cls) {
   rco_stats local;
   octx c;
   memset(&c, 0, sizeof c);
@@ -390,6 +395,7 @@ int rco_render(const json_data_t *js, int width, int height, int max_recursion, 
       float *cin = carry_in ? &carry_in[3 * ((size_t)y * width + x)] : NULL;
       if (cin) cin[0] = cin[1] = cin[2] = 0.0f;
       o_shoot(&c, d, max_recursion, mode, col, &pi, cin);
+      if (cls) cls[(size_t)y * width + x] = (uint8_t)(pi.dep ? (pi.wrote ? 3 : 2) : (pi.wrote ? 1 : 0));
       if (pi.dep) {
         c.st->dep_pixels++;
         if (pi.wrote) c.st->dep_writers++;

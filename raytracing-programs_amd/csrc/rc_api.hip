@@ -316,6 +316,22 @@ void fill_device_timing(DevCtx& c, const rc_options* opt, rc_timing* t) {
         }
         std::fclose(f);
       }
+      {   // per-round team log (k_resolve, team blocks)
+        std::vector<unsigned> tl(8 * 8192);
+        (void)hipMemcpy(tl.data(),
+                        (const unsigned*)c.trace.p + 3 * (size_t)cnt[2] + 4 * (size_t)cnt[0],
+                        tl.size() * sizeof(unsigned), hipMemcpyDeviceToHost);
+        std::string p3 = std::string(path) + ".team";
+        if (FILE* f = std::fopen(p3.c_str(), "w")) {
+          std::fprintf(f, "# round mode(0 scan/1 resolve) j0 j1 cycles lane_passes coop_steps changers\n");
+          for (int r = 1; r < 8192; ++r)
+            if (tl[8 * r + 7] == 0xA5A5A5A5u)
+              std::fprintf(f, "%d %u %u %u %u %u %u %u\n", r, tl[8 * r], tl[8 * r + 1],
+                           tl[8 * r + 2], tl[8 * r + 3], tl[8 * r + 4], tl[8 * r + 5],
+                           tl[8 * r + 6]);
+          std::fclose(f);
+        }
+      }
 #if RC_STAMPS
       std::vector<unsigned> sp(4 * (size_t)cnt[0]);
       (void)hipMemcpy(sp.data(), (const unsigned*)c.trace.p + 3 * (size_t)cnt[2],

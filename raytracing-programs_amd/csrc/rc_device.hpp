@@ -64,25 +64,57 @@ __device__ __forceinline__ float dot(V3 a, V3 b) {
 }
 __device__ __forceinline__ V3 sub(V3 a, V3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
 
+// Correctly rounded f64 sqrt for s = +-0, s >= 2^-767, +inf or NaN — every value it is used
+// on here: sums of squares of floats (0 or >= 2^-298) and non-negative floats widened to
+// double (0 or >= 2^-149).  This is the compiler's own rsq + Goldschmidt/Newton sequence
+// without its range scaling, which it applies only below 2^-767, so results are identical.
+__device__ __forceinline__ double sqrt_ns(double s) {
+  const double y = __builtin_amdgcn_rsq(s);
+  double g = s * y, h = y * 0.5;
+  const double r = __builtin_fma(-h, g, 0.5);
+  g = __builtin_fma(g, r, g);
+  h = __builtin_fma(h, r, h);
+  double d = __builtin_fma(-g, g, s);
+  g = __builtin_fma(d, h, g);
+  d = __builtin_fma(-g, g, s);
+  g = __builtin_fma(d, h, g);
+  return (s == 0.0 || s == __builtin_inf()) ? s : g;
+}
+
 // C/v3math.c:169-172 — (float)sqrt of an exact double sum of squares
 __device__ __forceinline__ float length(V3 a) {
   double s = (double)a.x * (double)a.x;
   s = s + (double)a.y * (double)a.y;
   s = s + (double)a.z * (double)a.z;
-  return (float)__builtin_sqrt(s);
+  return (float)sqrt_ns(s);
+}
+
+// a_i / len for the three components through one f64 reciprocal: r = 1/len to within
+// 2^-52 (rcp + two Newton steps), q = (double)a_i * r within 2^-51.4 of a_i/len.  A quotient
+// of two 24-bit floats is either a float or at least 2^-49 (relative) away from every
+// rounding midpoint of the float grid, so RN32(q) = RN32(a_i/len), the IEEE f32 quotient.
+// len = +inf: r = 0 gives a_i/inf (+-0, NaN for inf a_i); len NaN gives NaN; len = 0 is the
+// caller's case.
+__device__ __forceinline__ V3 div3(V3 a, float len) {
+  const double L = (double)len;
+  double r = __builtin_amdgcn_rcp(L);
+  double e = __builtin_fma(-L, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  e = __builtin_fma(-L, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  r = len == __builtin_inff() ? 0.0 : r;
+  return v3((float)((double)a.x * r), (float)((double)a.y * r), (float)((double)a.z * r));
 }
 
 // C/v3math.c:180-192 — a zero length leaves the vector unchanged (and is counted: the
-// reference prints a stderr line per event).  (A shared-reciprocal variant — provably exact
-// for float quotients, q = RN32((double)a * r) — was measured slower on gfx950: v_rcp_f64 and
-// the extra f64 ops cost more latency than three full-rate IEEE f32 divisions.)
+// reference prints a stderr line per event).
 __device__ __forceinline__ V3 normalize(V3 a, int& zero_events) {
   float len = length(a);
   if (len == 0.0f) {
     zero_events++;
     return a;
   }
-  return v3(a.x / len, a.y / len, a.z / len);
+  return div3(a, len);
 }
 
 // C/v3math.c:144-160 — v - n*(2*dot(v,n))
@@ -160,7 +192,7 @@ __device__ __forceinline__ bool hit_sphere(V3 O, V3 D, const rc_shape& s, RayK k
   float fac = k.a4 * c;
   float disc = (float)((double)b * (double)b - (double)fac);
   if (disc < 0.0f) return false;
-  double sq = __builtin_sqrt((double)disc);
+  double sq = sqrt_ns((double)disc);
   float tt = (float)(((double)(-b) - sq) / k.den);
   if (tt < 0.0f) tt = (float)(((double)(-b) + sq) / k.den);
   t = tt;
@@ -220,7 +252,7 @@ __device__ __forceinline__ bool hit_quadric(V3 O, V3 D, const rc_shape& q, float
   const float disc = (float)((double)bq * (double)bq - 4.0 * (double)aq * (double)cq);
   if ((double)disc < 0.0) return false;
   const double den = 2.0 * (double)aq;
-  const double sq = __builtin_sqrt((double)disc);
+  const double sq = sqrt_ns((double)disc);
   float tt = (float)(((double)(-bq) - sq) / den);
   if (tt <= 0.0f) tt = (float)(((double)(-bq) + sq) / den);
   t = tt;
@@ -636,7 +668,8 @@ __device__ __forceinline__ V3 sel(bool p, V3 a, V3 b) {
 
 __device__ __forceinline__ V3 normalize_sel(V3 a) {
   const float len = length(a);
-  return sel(len == 0.0f, a, v3(pin(a.x / len), pin(a.y / len), pin(a.z / len)));
+  const V3 q = div3(a, len);
+  return sel(len == 0.0f, a, v3(pin(q.x), pin(q.y), pin(q.z)));
 }
 
 // test_shape() for any type, branch-free.
@@ -688,7 +721,7 @@ __device__ __forceinline__ bool test_unified(const rc_shape& s, V3 O, V3 D, RayK
   // shared tail: one sqrt, two quotients
   const float B = isS ? bS : bq;
   const float disc = isS ? discS : discQ;
-  const double sq = pin(__builtin_sqrt((double)disc));
+  const double sq = pin(sqrt_ns((double)disc));
   const double nb = (double)(-B);
   const bool qlin = isQ & lin;
   const double n1q = pin(nb - sq), n1l = pin(-1.0 * (double)cq), n1p = pin((double)(-numP));

@@ -383,10 +383,15 @@ __device__ __forceinline__ DepRec shfl_rec(const DepRec& r, int src) {
 // the carry).  A changer found by a LANE pass switches to COOP; two clean COOP steps in a row
 // switch back.  `dense` carries the mode into the next window.  Returns the number of
 // evaluation steps; *changed tells whether any entry of the window moved the carry.
+struct WinStats {
+  int lane, coop, changers;
+};
+
 __device__ __forceinline__ int wave_window(const Scene& sc, int maxrec,
                                            const DepRec* __restrict__ dep_rec, int base,
                                            int end, V3& c, V3& mine, const LaneShape& ls,
-                                           int G, bool& dense, bool& changed
+                                           int G, bool& dense, bool& changed,
+                                           WinStats& ws
 #if RC_STAMPS
                                            , Stamps* st_
 #endif
@@ -411,6 +416,7 @@ __device__ __forceinline__ int wave_window(const Scene& sc, int maxrec,
   while (pos < nvalid) {
     ++evals;
     if (!coop) {
+      ++ws.lane;
       const bool act = valid && lane >= pos;
       V3 o = c;
       if (act) o = carry_path(sc, r, maxrec, c, zero);
@@ -425,10 +431,12 @@ __device__ __forceinline__ int wave_window(const Scene& sc, int maxrec,
       c = v3(__shfl(o.x, k, 64), __shfl(o.y, k, 64), __shfl(o.z, k, 64));
       pos = k + 1;
       changed = true;
+      ++ws.changers;
       coop = G > 0;
       clean_run = 0;
       continue;
     }
+    ++ws.coop;
     const int i = pos + e;
     const bool act = e < E && i < nvalid;
     const DepRec ri = shfl_rec(r, i < 64 ? i : 63);
@@ -459,6 +467,7 @@ __device__ __forceinline__ int wave_window(const Scene& sc, int maxrec,
     c = v3(__shfl(oc.x, g * GE, 64), __shfl(oc.y, g * GE, 64), __shfl(oc.z, g * GE, 64));
     pos += g + 1;
     changed = true;
+    ++ws.changers;
     clean_run = 0;
   }
   dense = coop;
@@ -585,6 +594,10 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
       while (j < end) {
         ++round;
         ++rounds_here;
+        const unsigned long long c_round = __builtin_amdgcn_s_memtime();
+        const int j_round = j;
+        WinStats tws = {0, 0, 0};
+        const bool was_resolve = resolve;
         if (!resolve) {
           // ---------------------------------------------------------------- SCAN
           const int base = j + ((int)blockIdx.x * 4 + wave) * 64;
@@ -652,7 +665,7 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
             while (j < end) {
               V3 mine;
               bool changed;
-              wave_window(sc, maxrec, dep_rec, j, end, c, mine, ls, G, dense, changed
+              wave_window(sc, maxrec, dep_rec, j, end, c, mine, ls, G, dense, changed, tws
 #if RC_STAMPS
                           , &stp
 #endif
@@ -679,6 +692,18 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
           resolve = false;
           __syncthreads();
         }
+        // debug trace: per-round team log after the per-segment records and stamps
+        if (trace && blockIdx.x == 0 && wave == 0 && lane == 0 && round < 8192) {
+          unsigned* tl = trace + 3 * (size_t)ndep + 4 * (size_t)nseg + 8 * (size_t)round;
+          tl[0] = was_resolve ? 1u : 0u;
+          tl[1] = (unsigned)j_round;
+          tl[2] = (unsigned)j;
+          tl[3] = (unsigned)(__builtin_amdgcn_s_memtime() - c_round);
+          tl[4] = (unsigned)tws.lane;
+          tl[5] = (unsigned)tws.coop;
+          tl[6] = (unsigned)tws.changers;
+          tl[7] = 0xA5A5A5A5u;
+        }
       }
       if (trace && blockIdx.x == 0 && threadIdx.x == 0) {
         trace[3 * s] = (unsigned)(__builtin_amdgcn_s_memrealtime() - t_seg);
@@ -703,10 +728,11 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
     int iters = 0;
     V3 c = seg_init_carry(dep_key, wcarry, start);
     bool dense = false;
+    WinStats ws = {0, 0, 0};
     for (int j = start; j < end; j += 64) {
       V3 mine;
       bool changed;
-      iters += wave_window(sc, maxrec, dep_rec, j, end, c, mine, ls, G, dense, changed
+      iters += wave_window(sc, maxrec, dep_rec, j, end, c, mine, ls, G, dense, changed, ws
 #if RC_STAMPS
                            , &stp
 #endif
