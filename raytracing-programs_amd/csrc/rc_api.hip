@@ -228,7 +228,8 @@ int ensure_parity(DevCtx& c, int W, int H, rc::ParityWork& w) {
   if (w.team_blocks > 256) w.team_blocks = 256;
   if (w.team_blocks > w.resolve_blocks / 2) w.team_blocks = w.resolve_blocks / 2;
   w.long_len = std::getenv("RC_LONG_LEN") ? std::atoi(std::getenv("RC_LONG_LEN")) : 32768;
-  w.team_coop = std::getenv("RC_TEAM_MODE") ? std::atoi(std::getenv("RC_TEAM_MODE")) : 1;
+  w.wave_k = std::getenv("RC_WAVE_K") ? std::atoi(std::getenv("RC_WAVE_K")) : 2;
+  w.resolve_k = std::getenv("RC_RESOLVE_K") ? std::atoi(std::getenv("RC_RESOLVE_K")) : 1;
   w.coop_group = 0;
   if (!std::getenv("RC_NO_COOP") && c.scene_src) {
     const int n = ((const rc_packed_header*)c.scene_src)->n;

@@ -44,7 +44,8 @@ struct ParityWork {
   int team_blocks;          // workgroups in the long-segment team (0: no team)
   int long_len;             // segments with >= long_len entries go to the team
   int phase_c_blocks;       // grid-stride phase C grid
-  int team_coop;            // team rounds use the cooperative evaluator
+  int wave_k;               // clean cooperative steps before a wave window goes back to LANE
+  int resolve_k;            // the same for the team leader's block window
   int coop_group;           // lanes per entry of the cooperative evaluator (0: off)
   unsigned* trace;          // optional [2*nseg] per-segment {ticks, evals} (debug)
 };

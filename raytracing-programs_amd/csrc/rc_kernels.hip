@@ -391,7 +391,7 @@ __device__ __forceinline__ int wave_window(const Scene& sc, int maxrec,
                                            const DepRec* __restrict__ dep_rec, int base,
                                            int end, V3& c, V3& mine, const LaneShape& ls,
                                            int G, bool& dense, bool& changed,
-                                           WinStats& ws
+                                           WinStats& ws, int K
 #if RC_STAMPS
                                            , Stamps* st_
 #endif
@@ -459,7 +459,7 @@ __device__ __forceinline__ int wave_window(const Scene& sc, int maxrec,
       const int lim = pos + E < nvalid ? pos + E : nvalid;
       if (lane >= pos && lane < lim) mine = c;
       pos = lim;
-      if (++clean_run >= 2) coop = false;
+      if (++clean_run >= K) coop = false;
       continue;
     }
     const int g = (__ffsll((long long)mc) - 1) / GE;
@@ -472,6 +472,110 @@ __device__ __forceinline__ int wave_window(const Scene& sc, int maxrec,
   }
   dense = coop;
   return evals;
+}
+
+// Block-level window for the team's RESOLVE leader: the 4 waves of one block resolve up to
+// 256 entries at the block-uniform carry c with the same LANE/COOP state machine as
+// wave_window, at 4x the width — COOP steps take 4*E entries (E per wave) and LANE passes
+// 256 — so clusters with short clean gaps cost one cooperative evaluation per changer.
+// The window's records sit in LDS (`rec`, loaded by the caller); per-step results meet in
+// double-buffered per-wave slots behind one barrier.  Entries are written to cin as they
+// resolve.  Every thread of the block must call this.
+struct BlockWinShared {
+  DepRec rec[kResolveBlock];
+  int wpos[2][4];
+  float wout[2][4][3];
+};
+
+__device__ __forceinline__ void block_window(const Scene& sc, int maxrec, BlockWinShared& bw,
+                                             int base, int nvalid, V3& c, const LaneShape& ls,
+                                             int G, bool& dense, bool& changed, int K,
+                                             float4* __restrict__ cin, WinStats& ws) {
+  constexpr int kNo = 0x7fffffff;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  changed = false;
+  int zero = 0;
+  int pos = 0;
+  int par = 0;
+  bool coop = dense && G > 0;
+  int clean_run = 0;
+  const bool spec = 2 * G <= 64;
+  const int GE = G > 0 ? (spec ? 2 * G : G) : 64;
+  const int E = 64 / GE;
+  const int Eb = 4 * E;
+  const int e = lane / GE, kself = G > 0 ? lane % G : 0, half = spec ? (lane / G) & 1 : 0;
+  while (pos < nvalid) {
+    int last;      // entries [pos, last] resolve with carry c
+    V3 cn = c;
+    bool hit;
+    if (!coop) {
+      ++ws.lane;
+      const bool act = t >= pos && t < nvalid;
+      V3 o = c;
+      if (act) o = carry_path(sc, bw.rec[t], maxrec, c, zero);
+      const unsigned long long m = __ballot(act && !same_bits(o, c));
+      const int k = m ? __ffsll((long long)m) - 1 : -1;
+      if (lane == 0) bw.wpos[par][wave] = k >= 0 ? wave * 64 + k : kNo;
+      if (k >= 0 && lane == k) {
+        bw.wout[par][wave][0] = o.x;
+        bw.wout[par][wave][1] = o.y;
+        bw.wout[par][wave][2] = o.z;
+      }
+    } else {
+      ++ws.coop;
+      const int i = pos + wave * E + e;
+      const bool act = e < E && i < nvalid;
+      const DepRec ri = bw.rec[i < nvalid ? i : pos];
+      V3 oc = c;
+#define RC_SPEC(GT) carry_path_spec<GT>(sc, ls, kself, G, half, ri, maxrec, c, zero)
+      if (act) {
+        if (G == 8) oc = RC_SPEC(8);
+        else if (G == 4) oc = RC_SPEC(4);
+        else if (G == 16) oc = RC_SPEC(16);
+        else if (spec) oc = RC_SPEC(0);
+        else oc = carry_path_coop(sc, ls, kself, G, ri, maxrec, c, zero);
+      }
+#undef RC_SPEC
+      const unsigned long long mc = __ballot(act && (lane % GE) == 0 && !same_bits(oc, c));
+      const int g = mc ? (__ffsll((long long)mc) - 1) / GE : -1;
+      if (lane == 0) bw.wpos[par][wave] = g >= 0 ? pos + wave * E + g : kNo;
+      if (g >= 0 && lane == g * GE) {
+        bw.wout[par][wave][0] = oc.x;
+        bw.wout[par][wave][1] = oc.y;
+        bw.wout[par][wave][2] = oc.z;
+      }
+    }
+    __syncthreads();
+    int wb = 0;
+    int best = bw.wpos[par][0];
+    for (int q = 1; q < 4; ++q) {
+      const int v = bw.wpos[par][q];
+      if (v < best) {
+        best = v;
+        wb = q;
+      }
+    }
+    hit = best != kNo;
+    if (hit) {
+      last = best;
+      cn = v3(bw.wout[par][wb][0], bw.wout[par][wb][1], bw.wout[par][wb][2]);
+    } else {
+      last = coop ? (pos + Eb < nvalid ? pos + Eb : nvalid) - 1 : nvalid - 1;
+    }
+    if (t >= pos && t <= last) cin[base + t] = make_float4(c.x, c.y, c.z, 0.0f);
+    pos = last + 1;
+    c = cn;
+    par ^= 1;
+    if (hit) {
+      changed = true;
+      ++ws.changers;
+      coop = G > 0;
+      clean_run = 0;
+    } else if (coop) {
+      if (++clean_run >= K) coop = false;
+    }
+  }
+  dense = coop;
 }
 
 // Team hand-off by data-tagged 8-byte granules (MI355X_MICROARCH.md: granule hand-off, R2):
@@ -536,7 +640,7 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
     const long long* __restrict__ dep_key, const float4* __restrict__ wcarry,
     const int* __restrict__ seg_start, const int* __restrict__ counters, int* __restrict__ head,
     float4* __restrict__ cin, int team_blocks, int long_len, TeamState* __restrict__ ts,
-    unsigned* __restrict__ trace, int G, int team_coop) {
+    unsigned* __restrict__ trace, int G, int wave_k, int resolve_k) {
   const int nseg = counters[0];
   const int ndep = counters[2];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -576,6 +680,7 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
     //            back to the team.
     __shared__ int s_pos[4];
     __shared__ float s_o[4][3];
+    __shared__ BlockWinShared s_bw;
     __shared__ int s_gpos;
     __shared__ float s_nc[3];
     const int T = team_blocks;
@@ -660,21 +765,27 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
           __syncthreads();
         } else {
           // ------------------------------------------------------------- RESOLVE
-          if (blockIdx.x == 0 && wave == 0) {
+          if (blockIdx.x == 0) {
             bool dense = true;   // the cluster starts right after a changer
+            // records of the first window; later windows are prefetched one ahead
+            const int t = threadIdx.x;
+            if (j + t < end) s_bw.rec[t] = dep_rec[j + t];
+            __syncthreads();
             while (j < end) {
-              V3 mine;
+              const int nv = end - j < kResolveBlock ? end - j : kResolveBlock;
+              DepRec nxt;
+              const int jn = j + nv;
+              if (jn + t < end) nxt = dep_rec[jn + t];
               bool changed;
-              wave_window(sc, maxrec, dep_rec, j, end, c, mine, ls, G, dense, changed, tws
-#if RC_STAMPS
-                          , &stp
-#endif
-                          );
-              if (j + lane < end) cin[j + lane] = make_float4(mine.x, mine.y, mine.z, 0.0f);
-              j = j + 64 < end ? j + 64 : end;
+              block_window(sc, maxrec, s_bw, j, nv, c, ls, G, dense, changed, resolve_k, cin,
+                           tws);
+              j = jn;
+              __syncthreads();   // everyone is done reading this window's records
               if (!changed) break;   // a clean window: the cluster is over
+              if (j + t < end) s_bw.rec[t] = nxt;
+              __syncthreads();
             }
-            if (lane == 0) team_publish(ts, round, (unsigned)j, c);
+            if (threadIdx.x == 0) team_publish(ts, round, (unsigned)j, c);
           }
           if (threadIdx.x == 0) {
             unsigned upos = 0;
@@ -732,7 +843,8 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
     for (int j = start; j < end; j += 64) {
       V3 mine;
       bool changed;
-      iters += wave_window(sc, maxrec, dep_rec, j, end, c, mine, ls, G, dense, changed, ws
+      iters += wave_window(sc, maxrec, dep_rec, j, end, c, mine, ls, G, dense, changed, ws,
+                           wave_k
 #if RC_STAMPS
                            , &stp
 #endif
@@ -838,7 +950,8 @@ hipError_t launch_parity(const LaunchScene& s, int W, int H, int maxrec, uint8_t
   hipLaunchKernelGGL(kres, dim3(w.resolve_blocks), dim3(kResolveBlock), w.resolve_lds, stream, sc,
                      maxrec, (const DepRec*)w.dep_rec, w.dep_key, w.wcarry, w.seg_start,
                      w.counters, w.counters + 1, w.cin, w.team_blocks, w.long_len,
-                     (TeamState*)w.team, w.trace, w.coop_group, w.team_coop);
+                     (TeamState*)w.team, w.trace, w.coop_group, w.wave_k,
+                     w.resolve_k);
   if (ev) (void)hipEventRecord(ev[2], stream);
   hipLaunchKernelGGL(k_phase_c, dim3(w.phase_c_blocks), dim3(kBlock), 0, stream, sc, cam, W,
                      maxrec, w.dep_pix, w.cin, w.counters + 2, out, zcount);
