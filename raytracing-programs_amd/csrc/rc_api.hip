@@ -72,6 +72,7 @@ struct DevCtx {
   const void* scene_src = nullptr;   // host image last uploaded
   // parity workspace
   DevBuf cls, wcarry, deprec, rows, dep_pix, dep_key, dep_rec, seg_flag, blk_cnt, seg_start,
+      seg_order,
       cin, counters, team, trace;
   int resident_blocks = 0;
   int resident_lds = -1;
@@ -192,6 +193,7 @@ int ensure_parity(DevCtx& c, int W, int H, rc::ParityWork& w) {
       c.dep_rec.ensure(P * rc::deprec_bytes()) || c.seg_flag.ensure(P) ||
       c.blk_cnt.ensure((P / 1024 + 2) * sizeof(int)) ||
       c.seg_start.ensure(P * sizeof(int)) || c.cin.ensure(P * sizeof(float4)) ||
+      c.seg_order.ensure((size_t)rc::kSegOrderMax * sizeof(int)) ||
       c.counters.ensure(64) || c.team.ensure(rc::team_state_bytes()))
     return -1;
   if (P >= (size_t)1 << 31) return -1;   // DEP indices are 32-bit
@@ -217,6 +219,7 @@ int ensure_parity(DevCtx& c, int W, int H, rc::ParityWork& w) {
   w.seg_flag = (uint8_t*)c.seg_flag.p;
   w.blk_cnt = (int*)c.blk_cnt.p;
   w.seg_start = (int*)c.seg_start.p;
+  w.seg_order = (int*)c.seg_order.p;
   w.cin = (float4*)c.cin.p;
   w.counters = (int*)c.counters.p;
   w.team = c.team.p;
@@ -316,6 +319,18 @@ void fill_device_timing(DevCtx& c, const rc_options* opt, rc_timing* t) {
                        tr[3 * k + 1], tr[3 * k + 2]);
         }
         std::fclose(f);
+      }
+      {   // per-segment start times (regular waves)
+        std::vector<unsigned> st(cnt[0]);
+        (void)hipMemcpy(st.data(),
+                        (const unsigned*)c.trace.p + 3 * (size_t)cnt[2] + 4 * (size_t)cnt[0] +
+                            8 * 8192,
+                        st.size() * sizeof(unsigned), hipMemcpyDeviceToHost);
+        std::string p4 = std::string(path) + ".start";
+        if (FILE* f = std::fopen(p4.c_str(), "w")) {
+          for (int k = 0; k < cnt[0]; ++k) std::fprintf(f, "%d %u\n", k, st[k]);
+          std::fclose(f);
+        }
       }
       {   // per-round team log (k_resolve, team blocks)
         std::vector<unsigned> tl(8 * 8192);

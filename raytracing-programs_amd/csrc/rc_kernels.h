@@ -37,7 +37,8 @@ struct ParityWork {
   int* blk_cnt;             // [P/1024] flag counts -> offsets
   int* seg_start;           // [P]   segment starts, in scan order
   float4* cin;              // [P]   resolved carry-in per DEP entry
-  int* counters;            // [4]   nseg, dequeue head, ndep, pad
+  int* counters;            // [4]   nseg, dequeue head, ndep, seg_order valid
+  int* seg_order;           // [kSegOrderMax] segments longest first (k_seg_order)
   void* team;               // TeamState of the long-segment team
   int resolve_blocks;       // persistent resolver grid (<= resident capacity)
   int resolve_lds;          // dynamic LDS per resolver block (occupancy control)
@@ -49,6 +50,8 @@ struct ParityWork {
   int coop_group;           // lanes per entry of the cooperative evaluator (0: off)
   unsigned* trace;          // optional [2*nseg] per-segment {ticks, evals} (debug)
 };
+
+constexpr int kSegOrderMax = 65536;   // segments ordered for the resolver queue (else FIFO)
 
 hipError_t launch_render(const LaunchScene& s, int W, int H, int row0, int row_step, int nrows,
                          int maxrec, uint8_t* out, unsigned long long* zcount,

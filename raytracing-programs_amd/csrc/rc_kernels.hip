@@ -474,6 +474,45 @@ __device__ __forceinline__ int wave_window(const Scene& sc, int maxrec,
   return evals;
 }
 
+// Resolver queue order: segments longest first (LPT), so the chains that take longest start
+// at once instead of after the queue reaches them.  One block: a counting sort into 256
+// length buckets of 32 entries (>= 8160 share the top bucket), stable within a bucket.
+// Above kSegOrderMax segments the queue stays in segment order (counters[3] = 0).
+__global__ void __launch_bounds__(1024) k_seg_order(const int* __restrict__ seg_start,
+                                                     int* __restrict__ counters,
+                                                     int* __restrict__ order) {
+  const int nseg = counters[0], ndep = counters[2];
+  if (nseg > kSegOrderMax) {
+    if (threadIdx.x == 0) counters[3] = 0;
+    return;
+  }
+  __shared__ int hist[256];
+  __shared__ int off[256];
+  const int t = threadIdx.x;
+  if (t < 256) hist[t] = 0;
+  __syncthreads();
+  auto bucket = [&](int s) {
+    const int len = (s + 1 < nseg ? seg_start[s + 1] : ndep) - seg_start[s];
+    const int b = len >> 5;
+    return 255 - (b < 255 ? b : 255);
+  };
+  // chunked so that the scatter below keeps segment order within a bucket
+  const int per = (nseg + 1023) / 1024;
+  const int s0 = t * per, s1 = s0 + per < nseg ? s0 + per : nseg;
+  for (int s = s0; s < s1; ++s) atomicAdd(&hist[bucket(s)], 1);
+  __syncthreads();
+  if (t == 0) {
+    int acc = 0;
+    for (int b = 0; b < 256; ++b) {
+      off[b] = acc;
+      acc += hist[b];
+    }
+  }
+  __syncthreads();
+  for (int s = s0; s < s1; ++s) order[atomicAdd(&off[bucket(s)], 1)] = s;
+  if (t == 0) counters[3] = 1;
+}
+
 // Block-level window for the team's RESOLVE leader: the 4 waves of one block resolve up to
 // 256 entries at the block-uniform carry c with the same LANE/COOP state machine as
 // wave_window, at 4x the width — COOP steps take 4*E entries (E per wave) and LANE passes
@@ -638,11 +677,13 @@ template <bool kLds>
 __global__ void __launch_bounds__(kResolveBlock) k_resolve(
     Scene sc, int maxrec, const DepRec* __restrict__ dep_rec,
     const long long* __restrict__ dep_key, const float4* __restrict__ wcarry,
-    const int* __restrict__ seg_start, const int* __restrict__ counters, int* __restrict__ head,
+    const int* __restrict__ seg_start, const int* __restrict__ seg_order,
+    const int* __restrict__ counters, int* __restrict__ head,
     float4* __restrict__ cin, int team_blocks, int long_len, TeamState* __restrict__ ts,
     unsigned* __restrict__ trace, int G, int wave_k, int resolve_k) {
   const int nseg = counters[0];
   const int ndep = counters[2];
+  const bool ordered = counters[3] != 0;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   // The chain steps read the winner's record (hit_frame) and refl[obj] every bounce level:
   // stage the shape records (n <= kLdsShapes) in LDS so those reads cost an LDS access
@@ -831,6 +872,7 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
     if (lane == 0) s = atomicAdd(head, 1);
     s = __shfl(s, 0, 64);
     if (s >= nseg) break;
+    if (ordered) s = seg_order[s];
     const int start = seg_start[s];
     const int end = (s + 1 < nseg) ? seg_start[s + 1] : ndep;
     if (team_blocks > 0 && end - start >= long_len) continue;
@@ -861,6 +903,8 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
       trace[3 * s] = (unsigned)(__builtin_amdgcn_s_memrealtime() - t_seg);
       trace[3 * s + 1] = (unsigned)iters;
       trace[3 * s + 2] = (unsigned)(__builtin_amdgcn_s_memtime() - c_seg);
+      // start time (low 32 bits of the 100 MHz clock) after the team log
+      trace[3 * (size_t)ndep + 4 * (size_t)nseg + 8 * 8192 + s] = (unsigned)t_seg;
     }
   }
 }
@@ -943,13 +987,15 @@ hipError_t launch_parity(const LaunchScene& s, int W, int H, int maxrec, uint8_t
                      w.counters + 0);
   hipLaunchKernelGGL(k_flag_scatter, dim3(nblk), dim3(kFlagBlock), 0, stream, w.seg_flag,
                      w.counters + 2, w.blk_cnt, w.seg_start);
+  hipLaunchKernelGGL(k_seg_order, dim3(1), dim3(1024), 0, stream, w.seg_start, w.counters,
+                     w.seg_order);
   // resolve_lds > 80 KiB keeps one resolver block (4 waves, one per SIMD) per CU: the chain
   // steps are latency-bound, so a resolver wave should not share its SIMD
   if (ev) (void)hipEventRecord(ev[1], stream);
   auto kres = s.n <= kLdsShapes ? k_resolve<true> : k_resolve<false>;
   hipLaunchKernelGGL(kres, dim3(w.resolve_blocks), dim3(kResolveBlock), w.resolve_lds, stream, sc,
                      maxrec, (const DepRec*)w.dep_rec, w.dep_key, w.wcarry, w.seg_start,
-                     w.counters, w.counters + 1, w.cin, w.team_blocks, w.long_len,
+                     w.seg_order, w.counters, w.counters + 1, w.cin, w.team_blocks, w.long_len,
                      (TeamState*)w.team, w.trace, w.coop_group, w.wave_k,
                      w.resolve_k);
   if (ev) (void)hipEventRecord(ev[2], stream);
