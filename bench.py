@@ -53,6 +53,23 @@ def load_pkg():
     return mod
 
 
+def pmc_traffic(kernel, scene, size, depth, mode):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of this
+    exact configuration (profiles/r01_pmc_traffic_<size>.json: 2*FETCH_SIZE + WRITE_SIZE, the
+    gfx950 correction of MI355X_MICROARCH.md); None when no profile covers it."""
+    path = os.path.join(ROOT, "profiles", f"r01_pmc_traffic_{size}.json")
+    if scene != "quadric" or depth != 6 or not os.path.exists(path):
+        return None, None
+    with open(path) as f:
+        prof = json.load(f)
+    if mode not in prof.get("config", ""):
+        return None, None
+    for name, d in prof["kernels"].items():
+        if name.split("::")[-1].split("<")[0] == kernel and "hbm_bytes" in d:
+            return d["hbm_bytes"], os.path.relpath(path, ROOT)
+    return None, None
+
+
 def cpu_baseline(scene_path, size, depth):
     """The reference itself (oracle/_ref/ref_timer_d<depth>: the C/ sources built like
     C/Makefile:4, raycast() timed alone) on the same image on one pinned host core; falls
@@ -169,6 +186,7 @@ def main():
             dom_flop = work["render_flop_per_px"] * W * nrows if work else None
             render_ms = phases["render_ms"]
         ach = dom_flop / (dom_ms * 1e-3) / 1e12 if dom_flop and dom_ms else None
+        traffic, traffic_src = pmc_traffic(dom_name, args.scene, args.size, args.depth, mode)
         rach = (work["render_flop_per_px"] * W * nrows / (render_ms * 1e-3) / 1e12
                 if work and render_ms else None)
         line = {
@@ -197,7 +215,9 @@ def main():
                          "achieved": round(ach, 4) if ach else None,
                          "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(ach / PEAK_FP64_TFLOPS, 5) if ach else None,
-                         "traffic": None,
+                         "traffic": traffic,
+                         "traffic_unit": "bytes per launch (HBM, PMC)",
+                         "traffic_source": traffic_src,
                          "note": ("serial carry chain: latency-bound, see DESIGN.md" if parity
                                   else "throughput kernel")},
             "roofline_render": {"bound": "valu",
