@@ -117,6 +117,26 @@ __device__ __forceinline__ V3 normalize(V3 a, int& zero_events) {
   return div3(a, len);
 }
 
+// Materialise a value in a register as an opaque definition.  Codegen otherwise turns a
+// select whose operand is an expensive single-use op (f64 division, sqrt) into a branch that
+// computes the operand conditionally, which serialises the independent quotients.
+template <class T>
+__device__ __forceinline__ T pin(T x) {
+  asm("" : "+v"(x));
+  return x;
+}
+
+// component-wise select (a struct-valued ?: becomes a pointer select over stack copies)
+__device__ __forceinline__ V3 sel(bool p, V3 a, V3 b) {
+  return v3(p ? a.x : b.x, p ? a.y : b.y, p ? a.z : b.z);
+}
+
+__device__ __forceinline__ V3 normalize_sel(V3 a) {
+  const float len = length(a);
+  const V3 q = div3(a, len);
+  return sel(len == 0.0f, a, v3(pin(q.x), pin(q.y), pin(q.z)));
+}
+
 // C/v3math.c:144-160 — v - n*(2*dot(v,n))
 __device__ __forceinline__ V3 reflect(V3 v, V3 n) {
   float s = 2.0f * dot(v, n);
@@ -409,11 +429,17 @@ __device__ __forceinline__ uint8_t quant(float c) {
 }
 
 // State a first-bounce-miss (DEP) pixel carries from phase A to phases B/C.
+// A DEP pixel's transfer-function inputs (48 B).  Neither bounce direction below depends on
+// the carry, so phase A computes them once: `a` = level 2's direction
+// normalize(reflect(d1, n0)), and `b` = level 3's direction if level 2 also misses,
+// normalize(reflect(a, n0)) (C/raycast.c:349-350 with the stale normal of a miss).
 struct DepRec {
-  float d1x, d1y, d1z;   // reflected direction of the missed first bounce
+  float ax, ay, az;      // level-2 direction
   float n0x, n0y, n0z;   // primary normal (misses never update the normal)
   int obj0;              // primary shape (stale object of the loop, C/raycast.c:359-362)
   int pad;
+  float bx, by, bz;      // level-3 direction when level 2 misses
+  int pad2;
 };
 
 struct PixelOut {
@@ -456,7 +482,9 @@ __device__ __forceinline__ void shoot(const Scene& sc, V3 d, int maxrec, V3 carr
       if (MODE == kModeFast) break;                     // CUDA/raycast.cu:224-237
       if (MODE == kModeParityA && lvl == 1) {
         po.cls = kClsDep;
-        po.dep = DepRec{D.x, D.y, D.z, N.x, N.y, N.z, obj, 0};
+        const V3 A = normalize_sel(reflect(D, N));
+        const V3 B = normalize_sel(reflect(A, N));
+        po.dep = DepRec{A.x, A.y, A.z, N.x, N.y, N.z, obj, 0, B.x, B.y, B.z, 0};
         return;
       }
     }
@@ -478,11 +506,11 @@ __device__ __forceinline__ void shoot(const Scene& sc, V3 d, int maxrec, V3 carr
 // phase-B transfer function f_p(c).  No shading: only the bounce-hit points matter.
 __device__ __forceinline__ V3 carry_path(const Scene& sc, const DepRec& r, int maxrec, V3 c,
                                          int& zero_events) {
-  V3 D = v3(r.d1x, r.d1y, r.d1z), N = v3(r.n0x, r.n0y, r.n0z), C = c;
+  V3 D = v3(r.ax, r.ay, r.az), N = v3(r.n0x, r.n0y, r.n0z), C = c;   // level 2's direction
   int obj = r.obj0, S = -1;
   for (int lvl = 2; lvl < maxrec; ++lvl) {
     if (!(sc.shapes[obj].refl > 0.0f)) break;
-    D = normalize(reflect(D, N), zero_events);
+    if (lvl > 2) D = normalize(reflect(D, N), zero_events);
     float t;
     const int i = nearest(sc, C, D, S, t);
     if (i >= 0) {
@@ -579,11 +607,11 @@ __device__ __forceinline__ V3 carry_path_coop(const Scene& sc, const LaneShape& 
                                               int G, const DepRec& r, int maxrec, V3 c,
                                               int& zero_events) {
   constexpr int kNone = 0x7fffffff;
-  V3 D = v3(r.d1x, r.d1y, r.d1z), N = v3(r.n0x, r.n0y, r.n0z), C = c;
+  V3 D = v3(r.ax, r.ay, r.az), N = v3(r.n0x, r.n0y, r.n0z), C = c;   // level 2's direction
   int obj = r.obj0, S = -1;
   for (int lvl = 2; lvl < maxrec; ++lvl) {
     if (!reflective(sc, obj)) break;
-    D = normalize(reflect(D, N), zero_events);
+    if (lvl > 2) D = normalize(reflect(D, N), zero_events);
     const RayK rk = ray_consts(D);
     float t = __builtin_inff();
     int k = kNone;
@@ -652,26 +680,6 @@ __device__ __forceinline__ unsigned long long stamp_now() {
 
 // normalize() without the branch (the zero-length case keeps the input, not counted: only
 // the final shading pass counts events).
-// Materialise a value in a register as an opaque definition.  Codegen otherwise turns a
-// select whose operand is an expensive single-use op (f64 division, sqrt) into a branch that
-// computes the operand conditionally, which serialises the independent quotients.
-template <class T>
-__device__ __forceinline__ T pin(T x) {
-  asm("" : "+v"(x));
-  return x;
-}
-
-// component-wise select (a struct-valued ?: becomes a pointer select over stack copies)
-__device__ __forceinline__ V3 sel(bool p, V3 a, V3 b) {
-  return v3(p ? a.x : b.x, p ? a.y : b.y, p ? a.z : b.z);
-}
-
-__device__ __forceinline__ V3 normalize_sel(V3 a) {
-  const float len = length(a);
-  const V3 q = div3(a, len);
-  return sel(len == 0.0f, a, v3(pin(q.x), pin(q.y), pin(q.z)));
-}
-
 // test_shape() for any type, branch-free.
 __device__ __forceinline__ bool test_unified(const rc_shape& s, V3 O, V3 D, RayK rk, int skip,
                                              float& t) {
@@ -789,7 +797,10 @@ __device__ __forceinline__ V3 carry_path_spec(const Scene& sc, const LaneShape& 
   (void)zero_events;
   const int G = GT ? GT : Grt;
   constexpr int kNone = 0x7fffffff;
-  V3 D = v3(r.d1x, r.d1y, r.d1z), N = v3(r.n0x, r.n0y, r.n0z), C = c;
+  V3 N = v3(r.n0x, r.n0y, r.n0z), C = c;
+  // the first step's two directions come with the record; each later step's are computed
+  // at the end of the step before it
+  V3 D1 = v3(r.ax, r.ay, r.az), D2 = v3(r.bx, r.by, r.bz);
   int obj = r.obj0, S = -1;
   const int lane = threadIdx.x & 63;
   const int lead0 = lane & ~(2 * G - 1);   // group h=0 leader of this entry
@@ -797,9 +808,6 @@ __device__ __forceinline__ V3 carry_path_spec(const Scene& sc, const LaneShape& 
   int lvl = 2;
   while (lvl < maxrec) {
     if (!reflective(sc, obj)) break;
-    RC_STAMP(3);
-    const V3 D1 = normalize_sel(reflect(D, N));
-    const V3 D2 = normalize_sel(reflect(D1, N));
     RC_STAMP(0);
     const V3 myD = sel(half, D2, D1);
     const int myS = half ? -1 : S;
@@ -839,8 +847,11 @@ __device__ __forceinline__ V3 carry_path_spec(const Scene& sc, const LaneShape& 
     N = sel(hit, Nw, N);
     obj = hit ? w : obj;
     S = hit ? w : -1;
-    D = Dw;
     lvl += two ? 2 : 1;
+    if (lvl >= maxrec || !reflective(sc, obj)) break;
+    RC_STAMP(3);
+    D1 = normalize_sel(reflect(Dw, N));
+    D2 = normalize_sel(reflect(D1, N));
   }
   return C;
 }

@@ -366,14 +366,18 @@ __device__ __forceinline__ V3 seg_init_carry(const long long* __restrict__ dep_k
 // 64/G entries per step, shapes spread over the G lanes of each group.
 __device__ __forceinline__ DepRec shfl_rec(const DepRec& r, int src) {
   DepRec o;
-  o.d1x = __shfl(r.d1x, src, 64);
-  o.d1y = __shfl(r.d1y, src, 64);
-  o.d1z = __shfl(r.d1z, src, 64);
+  o.ax = __shfl(r.ax, src, 64);
+  o.ay = __shfl(r.ay, src, 64);
+  o.az = __shfl(r.az, src, 64);
   o.n0x = __shfl(r.n0x, src, 64);
   o.n0y = __shfl(r.n0y, src, 64);
   o.n0z = __shfl(r.n0z, src, 64);
   o.obj0 = __shfl(r.obj0, src, 64);
   o.pad = 0;
+  o.bx = __shfl(r.bx, src, 64);
+  o.by = __shfl(r.by, src, 64);
+  o.bz = __shfl(r.bz, src, 64);
+  o.pad2 = 0;
   return o;
 }
 
@@ -566,7 +570,12 @@ __device__ __forceinline__ void block_window(const Scene& sc, int maxrec, BlockW
       const bool act = e < E && i < nvalid;
       const DepRec ri = bw.rec[i < nvalid ? i : pos];
       V3 oc = c;
+#if RC_STAMPS
+      Stamps stq = {{0, 0, 0, 0}, 0};
+#define RC_SPEC(GT) carry_path_spec<GT>(sc, ls, kself, G, half, ri, maxrec, c, zero, &stq)
+#else
 #define RC_SPEC(GT) carry_path_spec<GT>(sc, ls, kself, G, half, ri, maxrec, c, zero)
+#endif
       if (act) {
         if (G == 8) oc = RC_SPEC(8);
         else if (G == 4) oc = RC_SPEC(4);
