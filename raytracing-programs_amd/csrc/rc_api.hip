@@ -58,6 +58,10 @@ struct DevBuf {
 struct DevCtx {
   bool init = false;
   int device = 0;
+  unsigned epoch = 0;   // carry-in tag of the last parity frame
+  hipStream_t side = nullptr;   // phase C's side stream
+  hipEvent_t fork = nullptr, join = nullptr;
+  int side_blocks = 0;
   int cus = 256;
   hipStream_t stream = nullptr;
   // event sets: [0] start, then per phase ends (fast: [1] = render; parity: [1] phase A,
@@ -72,7 +76,7 @@ struct DevCtx {
   const void* scene_src = nullptr;   // host image last uploaded
   // parity workspace
   DevBuf cls, wcarry, deprec, rows, dep_pix, dep_key, dep_rec, seg_flag, blk_cnt, seg_start,
-      seg_order,
+      seg_order, batch_state,
       cin, counters, team, trace;
   int resident_blocks = 0;
   int resident_lds = -1;
@@ -192,11 +196,22 @@ int ensure_parity(DevCtx& c, int W, int H, rc::ParityWork& w) {
       c.dep_pix.ensure(P * sizeof(long long)) || c.dep_key.ensure(P * sizeof(long long)) ||
       c.dep_rec.ensure(P * rc::deprec_bytes()) || c.seg_flag.ensure(P) ||
       c.blk_cnt.ensure((P / 1024 + 2) * sizeof(int)) ||
-      c.seg_start.ensure(P * sizeof(int)) || c.cin.ensure(P * sizeof(float4)) ||
+      c.seg_start.ensure(P * sizeof(int)) ||
       c.seg_order.ensure((size_t)rc::kSegOrderMax * sizeof(int)) ||
+      c.batch_state.ensure((P / 64 + 2) * sizeof(int)) ||
       c.counters.ensure(64) || c.team.ensure(rc::team_state_bytes()))
     return -1;
   if (P >= (size_t)1 << 31) return -1;   // DEP indices are 32-bit
+  // carry-ins are tagged with a per-frame epoch: a fresh buffer starts at tag 0, which no
+  // frame uses
+  if (c.cin.bytes < P * rc::kCinBytes) {
+    if (c.cin.ensure(P * rc::kCinBytes) || hipMemset(c.cin.p, 0, P * rc::kCinBytes) != hipSuccess)
+      return -1;
+  }
+  if (++c.epoch == 0) {   // wrapped: clear old tags once
+    if (hipMemset(c.cin.p, 0, c.cin.bytes) != hipSuccess) return -1;
+    c.epoch = 1;
+  }
   const int one_per_cu = std::getenv("RC_RESOLVE_SHARED") ? 0 : 1;
   const int lds = one_per_cu ? 96 * 1024 : 0;
   if (!c.resident_blocks || c.resident_lds != lds) {
@@ -220,7 +235,23 @@ int ensure_parity(DevCtx& c, int W, int H, rc::ParityWork& w) {
   w.blk_cnt = (int*)c.blk_cnt.p;
   w.seg_start = (int*)c.seg_start.p;
   w.seg_order = (int*)c.seg_order.p;
-  w.cin = (float4*)c.cin.p;
+  w.cin = c.cin.p;
+  w.batch_state = (int*)c.batch_state.p;
+  w.side = nullptr;
+  if (!std::getenv("RC_NO_SIDE")) {   // phase C overlapped with the resolver
+    if (!c.side) {
+      if (hipStreamCreateWithFlags(&c.side, hipStreamNonBlocking) != hipSuccess ||
+          hipEventCreateWithFlags(&c.fork, hipEventDisableTiming) != hipSuccess ||
+          hipEventCreateWithFlags(&c.join, hipEventDisableTiming) != hipSuccess)
+        return -1;
+      c.side_blocks = rc::phase_c_side_blocks(c.cus);
+    }
+    w.side = c.side;
+    w.fork = c.fork;
+    w.join = c.join;
+    w.side_blocks = c.side_blocks;
+  }
+  w.epoch = c.epoch;
   w.counters = (int*)c.counters.p;
   w.team = c.team.p;
   // The team spins on a counter barrier: its blocks (the first of the grid) and the grid as

@@ -36,8 +36,13 @@ struct ParityWork {
   uint8_t* seg_flag;        // [P]   1 where a segment starts
   int* blk_cnt;             // [P/1024] flag counts -> offsets
   int* seg_start;           // [P]   segment starts, in scan order
-  float4* cin;              // [P]   resolved carry-in per DEP entry
-  int* counters;            // [4]   nseg, dequeue head, ndep, seg_order valid
+  void* cin;                // [P]   resolved carry-in per DEP entry (CinG tagged granules)
+  int* counters;            // [8]   nseg, dequeue head, ndep, seg_order valid, tail cursor
+  int* batch_state;         // [P/64+1] phase-C batch claim words (0 free, 1 claimed)
+  hipStream_t side;         // phase C's side stream (null: phase C after the resolver only)
+  hipEvent_t fork, join;    // side stream waits on fork; the main stream waits on join
+  int side_blocks;          // resident k_phase_c_side workgroups
+  unsigned epoch;           // this frame's carry-in tag (never 0)
   int* seg_order;           // [kSegOrderMax] segments longest first (k_seg_order)
   void* team;               // TeamState of the long-segment team
   int resolve_blocks;       // persistent resolver grid (<= resident capacity)
@@ -52,6 +57,7 @@ struct ParityWork {
 };
 
 constexpr int kSegOrderMax = 65536;   // segments ordered for the resolver queue (else FIFO)
+constexpr int kCinBytes = 24;         // one carry-in = three tagged 8-byte granules
 
 hipError_t launch_render(const LaunchScene& s, int W, int H, int row0, int row_step, int nrows,
                          int maxrec, uint8_t* out, unsigned long long* zcount,
@@ -64,5 +70,6 @@ hipError_t launch_parity(const LaunchScene& s, int W, int H, int maxrec, uint8_t
 size_t deprec_bytes();
 size_t team_state_bytes();
 int resolve_blocks_resident(int cus, int lds_bytes);
+int phase_c_side_blocks(int cus);
 
 }  // namespace rc

@@ -478,14 +478,50 @@ __device__ __forceinline__ int wave_window(const Scene& sc, int maxrec,
   return evals;
 }
 
+__device__ __forceinline__ unsigned long long pack2(unsigned lo, unsigned hi) {
+  return (unsigned long long)lo | ((unsigned long long)hi << 32);
+}
+
+// Carry-in hand-off (MI355X_MICROARCH.md / cdna_hip_programming.md Guideline 16, R2): each
+// entry's carry-in is three naturally aligned 8-byte granules {value, tag}, each written by ONE
+// agent-scope (sc1) store, tag = this frame's epoch.  The phase-C tail (other waves of the same
+// launch, any XCD) reads them with sc1 loads and accepts an entry only when all three tags
+// match, so no flag, fence or ordering is involved; a stale or torn entry is simply retried.
+struct CinG {
+  unsigned long long g[3];
+};
+__device__ __forceinline__ void cin_put(CinG* cin, int j, V3 c, unsigned tag) {
+  __hip_atomic_store(&cin[j].g[0], pack2(__float_as_uint(c.x), tag), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(&cin[j].g[1], pack2(__float_as_uint(c.y), tag), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(&cin[j].g[2], pack2(__float_as_uint(c.z), tag), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ bool cin_get(CinG* cin, int j, unsigned tag, V3& c) {
+  const unsigned long long a =
+      __hip_atomic_load(&cin[j].g[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned long long b =
+      __hip_atomic_load(&cin[j].g[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned long long d =
+      __hip_atomic_load(&cin[j].g[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  c = v3(__uint_as_float((unsigned)a), __uint_as_float((unsigned)b),
+         __uint_as_float((unsigned)d));
+  return (unsigned)(a >> 32) == tag && (unsigned)(b >> 32) == tag &&
+         (unsigned)(d >> 32) == tag;
+}
+
 // Resolver queue order: segments longest first (LPT), so the chains that take longest start
 // at once instead of after the queue reaches them.  One block: a counting sort into 256
 // length buckets of 32 entries (>= 8160 share the top bucket), stable within a bucket.
 // Above kSegOrderMax segments the queue stays in segment order (counters[3] = 0).
 __global__ void __launch_bounds__(1024) k_seg_order(const int* __restrict__ seg_start,
                                                      int* __restrict__ counters,
-                                                     int* __restrict__ order) {
+                                                     int* __restrict__ order,
+                                                     int* __restrict__ batch_state) {
   const int nseg = counters[0], ndep = counters[2];
+  // phase C's per-batch claim words (64 DEP entries per batch), zeroed for this frame
+  for (int b = threadIdx.x; b < (ndep + 63) / 64; b += blockDim.x) batch_state[b] = 0;
   if (nseg > kSegOrderMax) {
     if (threadIdx.x == 0) counters[3] = 0;
     return;
@@ -533,7 +569,8 @@ struct BlockWinShared {
 __device__ __forceinline__ void block_window(const Scene& sc, int maxrec, BlockWinShared& bw,
                                              int base, int nvalid, V3& c, const LaneShape& ls,
                                              int G, bool& dense, bool& changed, int K,
-                                             float4* __restrict__ cin, WinStats& ws) {
+                                             CinG* __restrict__ cin, unsigned tag,
+                                             WinStats& ws) {
   constexpr int kNo = 0x7fffffff;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   changed = false;
@@ -610,7 +647,7 @@ __device__ __forceinline__ void block_window(const Scene& sc, int maxrec, BlockW
     } else {
       last = coop ? (pos + Eb < nvalid ? pos + Eb : nvalid) - 1 : nvalid - 1;
     }
-    if (t >= pos && t <= last) cin[base + t] = make_float4(c.x, c.y, c.z, 0.0f);
+    if (t >= pos && t <= last) cin_put(cin, base + t, c, tag);
     pos = last + 1;
     c = cn;
     par ^= 1;
@@ -635,9 +672,6 @@ __device__ __forceinline__ void block_window(const Scene& sc, int maxrec, BlockW
 struct alignas(32) TeamSlot {
   unsigned long long g[4];
 };
-__device__ __forceinline__ unsigned long long pack2(unsigned lo, unsigned hi) {
-  return (unsigned long long)lo | ((unsigned long long)hi << 32);
-}
 
 struct TeamState {
   int error;        // a granule spin timed out (5 s)
@@ -687,9 +721,12 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
     Scene sc, int maxrec, const DepRec* __restrict__ dep_rec,
     const long long* __restrict__ dep_key, const float4* __restrict__ wcarry,
     const int* __restrict__ seg_start, const int* __restrict__ seg_order,
-    const int* __restrict__ counters, int* __restrict__ head,
-    float4* __restrict__ cin, int team_blocks, int long_len, TeamState* __restrict__ ts,
-    unsigned* __restrict__ trace, int G, int wave_k, int resolve_k) {
+    int* __restrict__ counters, int* __restrict__ head,
+    CinG* __restrict__ cin, int team_blocks, int long_len, TeamState* __restrict__ ts,
+    unsigned* __restrict__ trace, int G, int wave_k, int resolve_k, unsigned tag) {
+  // census for phase C's side kernel: it only proceeds once every resolver block is resident
+  if (threadIdx.x == 0)
+    __hip_atomic_fetch_add(&counters[5], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int nseg = counters[0];
   const int ndep = counters[2];
   const bool ordered = counters[3] != 0;
@@ -804,7 +841,7 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
           __syncthreads();
           const int gpos = s_gpos;
           // entries before the first changer, and the changer itself, read carry c
-          if (valid && idx <= gpos) cin[idx] = make_float4(c.x, c.y, c.z, 0.0f);
+          if (valid && idx <= gpos) cin_put(cin, idx, c, tag);
           if (gpos == 0x7fffffff) {
             j += window;
           } else {
@@ -828,7 +865,7 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
               if (jn + t < end) nxt = dep_rec[jn + t];
               bool changed;
               block_window(sc, maxrec, s_bw, j, nv, c, ls, G, dense, changed, resolve_k, cin,
-                           tws);
+                           tag, tws);
               j = jn;
               __syncthreads();   // everyone is done reading this window's records
               if (!changed) break;   // a clean window: the cluster is over
@@ -900,7 +937,7 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
                            , &stp
 #endif
                            );
-      if (j + lane < end) cin[j + lane] = make_float4(mine.x, mine.y, mine.z, 0.0f);
+      if (j + lane < end) cin_put(cin, j + lane, mine, tag);
     }
 #if RC_STAMPS
     if (trace && lane == 0 && end - start > 1000) {
@@ -919,22 +956,122 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
 }
 
 // ------------------------------------------------------------------ parity phase C --
+// Phase C shades every DEP pixel with its resolved carry-in, in batches of 64 consecutive DEP
+// entries (one per lane).  It overlaps the resolver: k_phase_c_side runs on a second stream
+// and, through an LDS reservation larger than what a resolver workgroup leaves free on its
+// CU, only ever occupies CUs the resolver has left, so it never shares a SIMD with a carry
+// chain.  Pass 1 shades the batches whose carry-ins are already published (tagged granules,
+// CinG) and skips the rest; pass 2 takes every batch not yet claimed and waits for it.
+// k_phase_c, after the resolver on the main stream, claims whatever is left (nothing waits by
+// then).  A batch is shaded exactly once: its claim word goes 0 -> 1 by an agent-scope CAS.
+constexpr int kSideBlock = 256;
+constexpr int kSideLds = 65 * 1024;   // > 160 KiB - 96 KiB: never beside a resolver workgroup
+
+__device__ __forceinline__ bool batch_claim(int* state, int b) {
+  int expect = 0;
+  return __hip_atomic_compare_exchange_strong(&state[b], &expect, 1, __ATOMIC_RELAXED,
+                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Loads batch b's carry-ins; false if `wait` is false and one is not published yet.
+__device__ __forceinline__ bool batch_carries(CinG* cin, int ndep, int b, unsigned tag,
+                                              bool wait, V3& c, TeamState* ts) {
+  const int j = b * 64 + (int)(threadIdx.x & 63);
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  for (;;) {
+    bool ok = true;
+    if (j < ndep) ok = cin_get(cin, j, tag, c);
+    if (__all(ok)) return true;
+    if (!wait) return false;
+    if (__builtin_amdgcn_s_memrealtime() - t0 > 500000000ull) {   // 5 s
+      if ((threadIdx.x & 63) == 0)
+        __hip_atomic_store(&ts->error, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return true;
+    }
+    __builtin_amdgcn_s_sleep(32);
+  }
+}
+
+__device__ __forceinline__ void shade_batch(const Scene& sc, const Cam& cam, int W, int maxrec,
+                                            const long long* __restrict__ dep_pix, int ndep,
+                                            int b, V3 c, uint8_t* __restrict__ out,
+                                            int& zero) {
+  const int j = b * 64 + (int)(threadIdx.x & 63);
+  if (j >= ndep) return;
+  const long long p = dep_pix[j];
+  const int y = (int)(p / W), x = (int)(p % W);
+  const V3 d = primary_dir(cam, x, y, zero);
+  PixelOut po;
+  shoot<kModeParityC>(sc, d, maxrec, c, po, zero);
+  store_rgb(out + (size_t)p * 3, po.rgb);
+}
+
+__device__ __forceinline__ int wave_ticket(int* ctr) {
+  int b = 0;
+  if ((threadIdx.x & 63) == 0) b = atomicAdd(ctr, 1);
+  return __shfl(b, 0, 64);
+}
+
+__global__ void __launch_bounds__(kSideBlock) k_phase_c_side(
+    Scene sc, Cam cam, int W, int maxrec, const long long* __restrict__ dep_pix,
+    CinG* __restrict__ cin, int* __restrict__ counters, int* __restrict__ batch_state,
+    uint8_t* __restrict__ out, unsigned long long* __restrict__ zcount,
+    TeamState* __restrict__ ts, int resolve_blocks, unsigned tag) {
+  __shared__ int s_go;
+  // Until every resolver workgroup is resident this workgroup may be holding a CU one of
+  // them needs (the resolver's team spins on co-residency): leave instead of waiting.
+  if (threadIdx.x == 0)
+    s_go = __hip_atomic_load(&counters[5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >=
+           resolve_blocks;
+  __syncthreads();
+  if (!s_go) return;
+  const int nb = (counters[2] + 63) / 64;
+  const int ndep = counters[2];
+  int zero = 0;
+  for (;;) {   // pass 1: published batches only
+    const int b = wave_ticket(&counters[4]);
+    if (b >= nb) break;
+    V3 c = v3(0.0f, 0.0f, 0.0f);
+    if (!batch_carries(cin, ndep, b, tag, false, c, ts)) continue;
+    int mine = 0;
+    if ((threadIdx.x & 63) == 0) mine = batch_claim(batch_state, b);
+    if (!__shfl(mine, 0, 64)) continue;
+    shade_batch(sc, cam, W, maxrec, dep_pix, ndep, b, c, out, zero);
+  }
+  for (;;) {   // pass 2: everything still unclaimed, waiting for its carry-ins
+    const int b = wave_ticket(&counters[6]);
+    if (b >= nb) break;
+    int mine = 0;
+    if ((threadIdx.x & 63) == 0) mine = batch_claim(batch_state, b);
+    if (!__shfl(mine, 0, 64)) continue;
+    V3 c = v3(0.0f, 0.0f, 0.0f);
+    (void)batch_carries(cin, ndep, b, tag, true, c, ts);
+    shade_batch(sc, cam, W, maxrec, dep_pix, ndep, b, c, out, zero);
+  }
+  flush_events(zero, zcount);
+}
+
+// After the resolver: the batches phase C's side kernel has not claimed.
 __global__ void __launch_bounds__(kBlock) k_phase_c(Scene sc, Cam cam, int W, int maxrec,
                                                     const long long* __restrict__ dep_pix,
-                                                    const float4* __restrict__ cin,
-                                                    const int* __restrict__ ndep_p,
+                                                    CinG* __restrict__ cin,
+                                                    int* __restrict__ counters,
+                                                    int* __restrict__ batch_state,
                                                     uint8_t* __restrict__ out,
-                                                    unsigned long long* __restrict__ zcount) {
-  const int ndep = *ndep_p;
+                                                    unsigned long long* __restrict__ zcount,
+                                                    TeamState* __restrict__ ts, unsigned tag) {
+  const int ndep = counters[2];
+  const int nb = (ndep + 63) / 64;
   int zero = 0;
-  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < ndep; j += gridDim.x * blockDim.x) {
-    const long long p = dep_pix[j];
-    const int y = (int)(p / W), x = (int)(p % W);
-    const V3 d = primary_dir(cam, x, y, zero);
-    const float4 c4 = cin[j];
-    PixelOut po;
-    shoot<kModeParityC>(sc, d, maxrec, v3(c4.x, c4.y, c4.z), po, zero);
-    store_rgb(out + (size_t)p * 3, po.rgb);
+  for (;;) {
+    const int b = wave_ticket(&counters[6]);
+    if (b >= nb) break;
+    int mine = 0;
+    if ((threadIdx.x & 63) == 0) mine = batch_claim(batch_state, b);
+    if (!__shfl(mine, 0, 64)) continue;
+    V3 c = v3(0.0f, 0.0f, 0.0f);
+    (void)batch_carries(cin, ndep, b, tag, true, c, ts);
+    shade_batch(sc, cam, W, maxrec, dep_pix, ndep, b, c, out, zero);
   }
   flush_events(zero, zcount);
 }
@@ -980,7 +1117,7 @@ hipError_t launch_parity(const LaunchScene& s, int W, int H, int maxrec, uint8_t
   hipLaunchKernelGGL(k_phase_a, grid, dim3(kBlock), 0, stream, sc, cam, W, H, maxrec, out,
                      w.cls, w.wcarry, (DepRec*)w.deprec, zcount);
   if (ev) (void)hipEventRecord(ev[0], stream);
-  (void)hipMemsetAsync(w.counters, 0, 4 * sizeof(int), stream);   // nseg, head, ndep, pad
+  (void)hipMemsetAsync(w.counters, 0, 8 * sizeof(int), stream);   // nseg, head, ndep, ...
   (void)hipMemsetAsync(w.team, 0, sizeof(TeamState), stream);     // error + round tags
   hipLaunchKernelGGL(k_row_stats, dim3(H), dim3(kScanBlock), 0, stream, w.cls, W, w.row_ndep,
                      w.row_lastw, w.row_lastdep);
@@ -997,24 +1134,45 @@ hipError_t launch_parity(const LaunchScene& s, int W, int H, int maxrec, uint8_t
   hipLaunchKernelGGL(k_flag_scatter, dim3(nblk), dim3(kFlagBlock), 0, stream, w.seg_flag,
                      w.counters + 2, w.blk_cnt, w.seg_start);
   hipLaunchKernelGGL(k_seg_order, dim3(1), dim3(1024), 0, stream, w.seg_start, w.counters,
-                     w.seg_order);
+                     w.seg_order, w.batch_state);
   // resolve_lds > 80 KiB keeps one resolver block (4 waves, one per SIMD) per CU: the chain
   // steps are latency-bound, so a resolver wave should not share its SIMD
   if (ev) (void)hipEventRecord(ev[1], stream);
+  if (w.side) (void)hipEventRecord(w.fork, stream);
   auto kres = s.n <= kLdsShapes ? k_resolve<true> : k_resolve<false>;
   hipLaunchKernelGGL(kres, dim3(w.resolve_blocks), dim3(kResolveBlock), w.resolve_lds, stream, sc,
                      maxrec, (const DepRec*)w.dep_rec, w.dep_key, w.wcarry, w.seg_start,
-                     w.seg_order, w.counters, w.counters + 1, w.cin, w.team_blocks, w.long_len,
-                     (TeamState*)w.team, w.trace, w.coop_group, w.wave_k,
-                     w.resolve_k);
+                     w.seg_order, w.counters, w.counters + 1, (CinG*)w.cin, w.team_blocks,
+                     w.long_len, (TeamState*)w.team, w.trace, w.coop_group, w.wave_k,
+                     w.resolve_k, w.epoch);
+  if (w.side) {   // phase C beside the resolver, on the CUs it leaves
+    (void)hipStreamWaitEvent(w.side, w.fork, 0);
+    hipLaunchKernelGGL(k_phase_c_side, dim3(w.side_blocks), dim3(kSideBlock), kSideLds, w.side,
+                       sc, cam, W, maxrec, w.dep_pix, (CinG*)w.cin, w.counters, w.batch_state,
+                       out, zcount, (TeamState*)w.team, w.resolve_blocks, w.epoch);
+    (void)hipEventRecord(w.join, w.side);
+  }
   if (ev) (void)hipEventRecord(ev[2], stream);
   hipLaunchKernelGGL(k_phase_c, dim3(w.phase_c_blocks), dim3(kBlock), 0, stream, sc, cam, W,
-                     maxrec, w.dep_pix, w.cin, w.counters + 2, out, zcount);
+                     maxrec, w.dep_pix, (CinG*)w.cin, w.counters, w.batch_state, out, zcount,
+                     (TeamState*)w.team, w.epoch);
+  if (w.side) (void)hipStreamWaitEvent(stream, w.join, 0);
   if (ev) (void)hipEventRecord(ev[3], stream);
   return hipGetLastError();
 }
 
 size_t team_state_bytes() { return sizeof(TeamState); }
+
+int phase_c_side_blocks(int cus) {
+  (void)hipFuncSetAttribute((const void*)k_phase_c_side,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, kSideLds);
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_phase_c_side, kSideBlock,
+                                                   kSideLds) != hipSuccess ||
+      per_cu <= 0)
+    per_cu = 1;
+  return per_cu * cus;
+}
 
 int resolve_blocks_resident(int cus, int lds_bytes) {
   if (lds_bytes > 0) {
