@@ -314,6 +314,19 @@ int enqueue_render(DevCtx& c, const rc_scene* s, int W, int H, int row0, int row
   return 0;
 }
 
+// After a synchronised parity render: the resolver's and phase C's bounded spins set
+// TeamState.error (first word) if a hand-off never completed; the image is then invalid.
+int check_spin_error(DevCtx& c, const rc_options* opt) {
+  if (!(opt->mode == RC_MODE_PARITY && opt->max_recursion > 1) || !c.team.p) return 0;
+  int err = 0;
+  if (hipMemcpy(&err, c.team.p, sizeof err, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  if (err) {
+    std::fprintf(stderr, "Error: parity resolver hand-off timed out (code %d)\n", err);
+    return -1;
+  }
+  return 0;
+}
+
 double event_ms(hipEvent_t a, hipEvent_t b) {
   float ms = 0.0f;
   if (hipEventElapsedTime(&ms, a, b) != hipSuccess) return 0.0;
@@ -423,6 +436,7 @@ int rc_render_device(const rc_scene* s, int W, int H, int row0, int row_step, in
   if (timing) {
     std::memset(timing, 0, sizeof *timing);
     HIP_TRY(hipStreamSynchronize(st));
+    if (check_spin_error(*c, opt)) return -1;
     fill_device_timing(*c, opt, timing);
     timing->total_ms = timing->kernel_ms;
   }
@@ -518,6 +532,10 @@ int rc_render(const rc_scene* s, int W, int H, const rc_options* opt, uint8_t* p
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     if (e != hipSuccess) {
       std::fprintf(stderr, "Error: HIP copy failed: %s\n", hipGetErrorString(e));
+      rcodes[g] = -1;
+      return;
+    }
+    if (check_spin_error(*c, opt)) {
       rcodes[g] = -1;
       return;
     }

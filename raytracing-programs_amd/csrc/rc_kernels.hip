@@ -18,6 +18,10 @@
 #include "rc_device.hpp"
 #include "rc_kernels.h"
 
+#ifndef RC_PHASE_A_WAVES
+#define RC_PHASE_A_WAVES 4   // waves per SIMD the render kernels are compiled for
+#endif
+
 namespace rc {
 
 constexpr int kTile = 16;        // 16x16 pixels per workgroup, 256 lanes
@@ -40,7 +44,7 @@ __device__ __forceinline__ void flush_events(int zero_events, unsigned long long
 }
 
 // ------------------------------------------------------------------ fast / depth 0 --
-__global__ void __launch_bounds__(kBlock) k_render(Scene sc, Cam cam, int W, int H, int row0,
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_PHASE_A_WAVES))) k_render(Scene sc, Cam cam, int W, int H, int row0,
                                                    int row_step, int nrows, int maxrec,
                                                    uint8_t* __restrict__ out,
                                                    unsigned long long* __restrict__ zcount) {
@@ -59,7 +63,7 @@ __global__ void __launch_bounds__(kBlock) k_render(Scene sc, Cam cam, int W, int
 }
 
 // ------------------------------------------------------------------ parity phase A --
-__global__ void __launch_bounds__(kBlock) k_phase_a(Scene sc, Cam cam, int W, int H, int maxrec,
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_PHASE_A_WAVES))) k_phase_a(Scene sc, Cam cam, int W, int H, int maxrec,
                                                     uint8_t* __restrict__ out,
                                                     uint8_t* __restrict__ cls,
                                                     float4* __restrict__ wcarry,
@@ -1052,7 +1056,7 @@ __global__ void __launch_bounds__(kSideBlock) k_phase_c_side(
 }
 
 // After the resolver: the batches phase C's side kernel has not claimed.
-__global__ void __launch_bounds__(kBlock) k_phase_c(Scene sc, Cam cam, int W, int maxrec,
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) k_phase_c(Scene sc, Cam cam, int W, int maxrec,
                                                     const long long* __restrict__ dep_pix,
                                                     CinG* __restrict__ cin,
                                                     int* __restrict__ counters,
