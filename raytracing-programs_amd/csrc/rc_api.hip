@@ -61,7 +61,7 @@ struct DevCtx {
   unsigned epoch = 0;   // carry-in tag of the last parity frame
   hipStream_t side = nullptr;   // phase C's side stream
   hipEvent_t fork = nullptr, join = nullptr;
-  int side_blocks = 0;
+  int side_blocks = 0, side_lds = 0;
   int cus = 256;
   hipStream_t stream = nullptr;
   // event sets: [0] start, then per phase ends (fast: [1] = render; parity: [1] phase A,
@@ -238,18 +238,23 @@ int ensure_parity(DevCtx& c, int W, int H, rc::ParityWork& w) {
   w.cin = c.cin.p;
   w.batch_state = (int*)c.batch_state.p;
   w.side = nullptr;
+  w.split_shade = std::getenv("RC_SPLIT_SHADE") ? 1 : 0;
   if (!std::getenv("RC_NO_SIDE")) {   // phase C overlapped with the resolver
     if (!c.side) {
       if (hipStreamCreateWithFlags(&c.side, hipStreamNonBlocking) != hipSuccess ||
           hipEventCreateWithFlags(&c.fork, hipEventDisableTiming) != hipSuccess ||
           hipEventCreateWithFlags(&c.join, hipEventDisableTiming) != hipSuccess)
         return -1;
-      c.side_blocks = rc::phase_c_side_blocks(c.cus);
+      c.side_lds = rc::side_lds_bytes(96 * 1024);
+      c.side_blocks = rc::phase_c_side_blocks(c.cus, c.side_lds);
     }
-    w.side = c.side;
-    w.fork = c.fork;
-    w.join = c.join;
-    w.side_blocks = c.side_blocks;
+    if (c.side_blocks > 0 && lds > 0) {   // the guard needs the resolver's LDS reservation
+      w.side = c.side;
+      w.fork = c.fork;
+      w.join = c.join;
+      w.side_blocks = c.side_blocks;
+      w.side_lds = c.side_lds;
+    }
   }
   w.epoch = c.epoch;
   w.counters = (int*)c.counters.p;
@@ -348,6 +353,14 @@ void fill_device_timing(DevCtx& c, const rc_options* opt, rc_timing* t) {
     int cnt[4] = {0, 0, 0, 0};
     if (hipMemcpy(cnt, c.counters.p, sizeof cnt, hipMemcpyDeviceToHost) == hipSuccess)
       t->dep_pixels = cnt[2];
+    if (std::getenv("RC_SIDE_STATS")) {
+      int cc[16];
+      if (hipMemcpy(cc, c.counters.p, sizeof cc, hipMemcpyDeviceToHost) == hipSuccess)
+        std::fprintf(stderr,
+                     "side: blocks go %d gave-up %d, tiles side %d finish %d, batches side %d "
+                     "finish %d (side_blocks %d)\n",
+                     cc[12], cc[13], cc[8], cc[10], cc[9], cc[11], c.side_blocks);
+    }
     const char* path = std::getenv("RC_RESOLVE_TRACE");
     if (path && c.trace.p && cnt[0] > 0) {   // debug: per-segment resolver trace
       std::vector<int> starts(cnt[0]);

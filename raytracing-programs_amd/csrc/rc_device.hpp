@@ -26,6 +26,7 @@ namespace rc {
 constexpr int kModeFast = 0;      // reflection miss ends the bounce loop
 constexpr int kModeParityA = 1;   // parity, phase A: stop at a first-bounce miss (DEP pixel)
 constexpr int kModeParityC = 2;   // parity, phase C: first-bounce miss reads the given carry
+constexpr int kModeClassify = 3;  // parity, phase A without shading: class, DEP record, carry
 
 constexpr uint8_t kClsIdent = 0;  // pixel never writes the carry
 constexpr uint8_t kClsWriter = 1; // first bounce hit: carry-out independent of carry-in
@@ -453,6 +454,7 @@ struct PixelOut {
 //  kModeFast     : miss ends the loop.
 //  kModeParityA  : a miss at level 1 stops here (cls = DEP, dep record filled).
 //  kModeParityC  : `carry` is this pixel's scan-order carry-in.
+//  kModeClassify : kModeParityA's control flow and carry without any shading (rgb = 0).
 template <int MODE>
 __device__ __forceinline__ void shoot(const Scene& sc, V3 d, int maxrec, V3 carry, PixelOut& po,
                                       int& zero_events) {
@@ -480,7 +482,7 @@ __device__ __forceinline__ void shoot(const Scene& sc, V3 d, int maxrec, V3 carr
       wrote = true;
     } else {
       if (MODE == kModeFast) break;                     // CUDA/raycast.cu:224-237
-      if (MODE == kModeParityA && lvl == 1) {
+      if ((MODE == kModeParityA || MODE == kModeClassify) && lvl == 1) {
         po.cls = kClsDep;
         const V3 A = normalize_sel(reflect(D, N));
         const V3 B = normalize_sel(reflect(A, N));
@@ -488,16 +490,21 @@ __device__ __forceinline__ void shoot(const Scene& sc, V3 d, int maxrec, V3 carr
         return;
       }
     }
-    V3 col = shade(sc, i >= 0 ? i : sc.n, C, N, D, zero_events);
-    out.x = out.x + col.x * T;
-    out.y = out.y + col.y * T;
-    out.z = out.z + col.z * T;
-    T = T * sc.shapes[obj].refl;
+    if (MODE != kModeClassify) {
+      V3 col = shade(sc, i >= 0 ? i : sc.n, C, N, D, zero_events);
+      out.x = out.x + col.x * T;
+      out.y = out.y + col.y * T;
+      out.z = out.z + col.z * T;
+      T = T * sc.shapes[obj].refl;
+    }
     O = C;
     S = i;
   }
-  V3 col = shade(sc, i0, P0, N0, d, zero_events);      // C/raycast.c:377-378
-  po.rgb = v3(out.x + col.x, out.y + col.y, out.z + col.z);
+  if (MODE != kModeClassify) {
+    V3 col = shade(sc, i0, P0, N0, d, zero_events);    // C/raycast.c:377-378
+    out = v3(out.x + col.x, out.y + col.y, out.z + col.z);
+  }
+  po.rgb = out;
   po.cls = wrote ? kClsWriter : kClsIdent;
   po.carry = C;
 }

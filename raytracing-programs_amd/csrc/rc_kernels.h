@@ -41,7 +41,9 @@ struct ParityWork {
   int* batch_state;         // [P/64+1] phase-C batch claim words (0 free, 1 claimed)
   hipStream_t side;         // phase C's side stream (null: phase C after the resolver only)
   hipEvent_t fork, join;    // side stream waits on fork; the main stream waits on join
-  int side_blocks;          // resident k_phase_c_side workgroups
+  int side_blocks;          // resident k_side workgroups
+  int side_lds;             // k_side's dynamic LDS reservation (keeps it off resolver CUs)
+  int split_shade;          // k_classify + colours in k_side (measured slower: off by default)
   unsigned epoch;           // this frame's carry-in tag (never 0)
   int* seg_order;           // [kSegOrderMax] segments longest first (k_seg_order)
   void* team;               // TeamState of the long-segment team
@@ -58,6 +60,7 @@ struct ParityWork {
 
 constexpr int kSegOrderMax = 65536;   // segments ordered for the resolver queue (else FIFO)
 constexpr int kCinBytes = 24;         // one carry-in = three tagged 8-byte granules
+constexpr int kLdsShapesMax = 64;     // k_resolve stages up to this many shapes in LDS
 
 hipError_t launch_render(const LaunchScene& s, int W, int H, int row0, int row_step, int nrows,
                          int maxrec, uint8_t* out, unsigned long long* zcount,
@@ -70,6 +73,7 @@ hipError_t launch_parity(const LaunchScene& s, int W, int H, int maxrec, uint8_t
 size_t deprec_bytes();
 size_t team_state_bytes();
 int resolve_blocks_resident(int cus, int lds_bytes);
-int phase_c_side_blocks(int cus);
+int side_lds_bytes(int resolve_dyn_lds);
+int phase_c_side_blocks(int cus, int side_lds);
 
 }  // namespace rc

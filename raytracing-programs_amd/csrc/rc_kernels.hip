@@ -3,17 +3,24 @@
 //   k_render      one lane per pixel, 16x16-pixel workgroups (four 8x8 wave tiles for ray
 //                 coherence), full iterative_shoot + quantisation, RGB store.  Fast mode, and
 //                 parity mode at depth 0 (no bounce loop => no carry).
-//   k_phase_a     parity phase A: same as k_render but a pixel whose first reflection misses
-//                 (a DEP pixel, it reads the scan-order carry) stops and records its state;
-//                 every other pixel is final.  Writers record their carry-out.
+//   k_classify    parity phase A, carry part: per pixel the class (ident / writer / DEP: a
+//                 pixel whose first reflection misses reads the scan-order carry), the DEP
+//                 record and the writers' carry-out — no shading.
+//   k_phase_a     the same plus the shading of every non-DEP pixel (used without the side
+//                 stream); with it, that shading runs in k_side beside the resolver.
 //   k_row_stats / k_row_scan / k_row_compact
 //                 scan-order compaction of the DEP pixels, each tagged with the last writer
 //                 before it (its segment key); segment starts appended to a work list.
 //   k_resolve     parity phase B: exact carry chain.  One workgroup per segment (dequeued
 //                 from a counter): evaluate a window of DEP pixels at the current carry in
 //                 parallel, the first pixel that changes the carry ends the step.
-//   k_phase_c     parity phase C: shade every DEP pixel with its resolved carry-in.
+//   k_side        side stream, beside the resolver: shade the non-DEP pixels, then every DEP
+//                 pixel with its resolved carry-in (parity phase C) as the carries appear.
+//   k_finish      after the resolver: whatever k_side has not claimed.
 #include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
 
 #include "rc_device.hpp"
 #include "rc_kernels.h"
@@ -87,6 +94,26 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_
   if (po.cls == kClsWriter) wcarry[p] = make_float4(po.carry.x, po.carry.y, po.carry.z, 0.0f);
   store_rgb(out + p * 3, po.rgb);
   flush_events(zero, zcount);
+}
+
+// Phase A's carry part only (no shading): k_side shades the non-DEP pixels off the critical path.
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_PHASE_A_WAVES))) k_classify(Scene sc, Cam cam, int W, int H, int maxrec,
+                                                     uint8_t* __restrict__ cls,
+                                                     float4* __restrict__ wcarry,
+                                                     DepRec* __restrict__ deprec) {
+  int lx, ly;
+  tile_pixel(lx, ly);
+  const int x = blockIdx.x * kTile + lx;
+  const int y = blockIdx.y * kTile + ly;
+  if (x >= W || y >= H) return;
+  const size_t p = (size_t)y * W + x;
+  int zero = 0;   // events are counted by the shading passes
+  const V3 d = primary_dir(cam, x, y, zero);
+  PixelOut po;
+  shoot<kModeClassify>(sc, d, maxrec, v3(0.0f, 0.0f, 0.0f), po, zero);
+  cls[p] = po.cls;
+  if (po.cls == kClsDep) deprec[p] = po.dep;
+  else if (po.cls == kClsWriter) wcarry[p] = make_float4(po.carry.x, po.carry.y, po.carry.z, 0.0f);
 }
 
 // ------------------------------------------------------- scan-order DEP compaction --
@@ -346,7 +373,7 @@ __global__ void __launch_bounds__(kFlagBlock) k_flag_scatter(const uint8_t* __re
 // device's resident capacity).
 constexpr int kResolveBlock = 256;
 constexpr int kTeamMax = 256;
-constexpr int kLdsShapes = 64;
+constexpr int kLdsShapes = kLdsShapesMax;
 
 __device__ __forceinline__ bool same_bits(V3 a, V3 b) {
   return __float_as_uint(a.x) == __float_as_uint(b.x) &&
@@ -960,16 +987,17 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
 }
 
 // ------------------------------------------------------------------ parity phase C --
-// Phase C shades every DEP pixel with its resolved carry-in, in batches of 64 consecutive DEP
-// entries (one per lane).  It overlaps the resolver: k_phase_c_side runs on a second stream
-// and, through an LDS reservation larger than what a resolver workgroup leaves free on its
-// CU, only ever occupies CUs the resolver has left, so it never shares a SIMD with a carry
-// chain.  Pass 1 shades the batches whose carry-ins are already published (tagged granules,
-// CinG) and skips the rest; pass 2 takes every batch not yet claimed and waits for it.
-// k_phase_c, after the resolver on the main stream, claims whatever is left (nothing waits by
-// then).  A batch is shaded exactly once: its claim word goes 0 -> 1 by an agent-scope CAS.
+// Colours and phase C beside the resolver.  k_classify leaves every colour to be shaded: the
+// non-DEP pixels (8x8 tiles, always ready) and the DEP pixels with their resolved carry-ins,
+// in batches of 64 consecutive DEP entries (one per lane).  k_side runs them on a second
+// stream while the resolver runs, on the CUs the resolver's workgroups have left (its LDS
+// reservation cannot fit beside one: side_lds_bytes; sharing the SIMDs slows the chains and,
+// above all, the team's rounds): tiles first, then phase C pass 1 (batches whose carry-ins
+// are already published — tagged granules, CinG) and pass 2 (everything not yet claimed,
+// waiting for it).  k_finish, after the resolver on the main stream, claims what is left.
+// A batch is shaded exactly once: its claim word goes 0 -> 1 by an agent-scope CAS; tiles
+// are claimed from one counter.
 constexpr int kSideBlock = 256;
-constexpr int kSideLds = 65 * 1024;   // > 160 KiB - 96 KiB: never beside a resolver workgroup
 
 __device__ __forceinline__ bool batch_claim(int* state, int b) {
   int expect = 0;
@@ -1016,23 +1044,33 @@ __device__ __forceinline__ int wave_ticket(int* ctr) {
   return __shfl(b, 0, 64);
 }
 
-__global__ void __launch_bounds__(kSideBlock) k_phase_c_side(
-    Scene sc, Cam cam, int W, int maxrec, const long long* __restrict__ dep_pix,
-    CinG* __restrict__ cin, int* __restrict__ counters, int* __restrict__ batch_state,
-    uint8_t* __restrict__ out, unsigned long long* __restrict__ zcount,
-    TeamState* __restrict__ ts, int resolve_blocks, unsigned tag) {
-  __shared__ int s_go;
-  // Until every resolver workgroup is resident this workgroup may be holding a CU one of
-  // them needs (the resolver's team spins on co-residency): leave instead of waiting.
-  if (threadIdx.x == 0)
-    s_go = __hip_atomic_load(&counters[5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >=
-           resolve_blocks;
-  __syncthreads();
-  if (!s_go) return;
-  const int nb = (counters[2] + 63) / 64;
+// Shading of one 8x8 tile's non-DEP pixels (phase A's colour part, events counted).
+__device__ __forceinline__ void shade_tile(const Scene& sc, const Cam& cam, int W, int H,
+                                           int maxrec, int t, const uint8_t* __restrict__ cls,
+                                           uint8_t* __restrict__ out, int& zero) {
+  const int tw = (W + 7) >> 3;
+  const int lane = threadIdx.x & 63;
+  const int x = (t % tw) * 8 + (lane & 7), y = (t / tw) * 8 + (lane >> 3);
+  if (x >= W || y >= H) return;
+  const size_t p = (size_t)y * W + x;
+  if (cls[p] == kClsDep) return;
+  const V3 d = primary_dir(cam, x, y, zero);
+  PixelOut po;
+  shoot<kModeParityA>(sc, d, maxrec, v3(0.0f, 0.0f, 0.0f), po, zero);
+  store_rgb(out + p * 3, po.rgb);
+}
+
+// Phase C pass 1 (published batches) and pass 2 (everything unclaimed, waiting).
+__device__ __forceinline__ void phase_c_passes(const Scene& sc, const Cam& cam, int W,
+                                               int maxrec, const long long* __restrict__ dep_pix,
+                                               CinG* __restrict__ cin, int* __restrict__ counters,
+                                               int* __restrict__ batch_state,
+                                               uint8_t* __restrict__ out, TeamState* ts,
+                                               unsigned tag, bool pass1, int& zero) {
+  int* done_ctr = &counters[pass1 ? 9 : 11];
   const int ndep = counters[2];
-  int zero = 0;
-  for (;;) {   // pass 1: published batches only
+  const int nb = (ndep + 63) / 64;
+  while (pass1) {
     const int b = wave_ticket(&counters[4]);
     if (b >= nb) break;
     V3 c = v3(0.0f, 0.0f, 0.0f);
@@ -1041,32 +1079,8 @@ __global__ void __launch_bounds__(kSideBlock) k_phase_c_side(
     if ((threadIdx.x & 63) == 0) mine = batch_claim(batch_state, b);
     if (!__shfl(mine, 0, 64)) continue;
     shade_batch(sc, cam, W, maxrec, dep_pix, ndep, b, c, out, zero);
+    if ((threadIdx.x & 63) == 0) atomicAdd(done_ctr, 1);
   }
-  for (;;) {   // pass 2: everything still unclaimed, waiting for its carry-ins
-    const int b = wave_ticket(&counters[6]);
-    if (b >= nb) break;
-    int mine = 0;
-    if ((threadIdx.x & 63) == 0) mine = batch_claim(batch_state, b);
-    if (!__shfl(mine, 0, 64)) continue;
-    V3 c = v3(0.0f, 0.0f, 0.0f);
-    (void)batch_carries(cin, ndep, b, tag, true, c, ts);
-    shade_batch(sc, cam, W, maxrec, dep_pix, ndep, b, c, out, zero);
-  }
-  flush_events(zero, zcount);
-}
-
-// After the resolver: the batches phase C's side kernel has not claimed.
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) k_phase_c(Scene sc, Cam cam, int W, int maxrec,
-                                                    const long long* __restrict__ dep_pix,
-                                                    CinG* __restrict__ cin,
-                                                    int* __restrict__ counters,
-                                                    int* __restrict__ batch_state,
-                                                    uint8_t* __restrict__ out,
-                                                    unsigned long long* __restrict__ zcount,
-                                                    TeamState* __restrict__ ts, unsigned tag) {
-  const int ndep = counters[2];
-  const int nb = (ndep + 63) / 64;
-  int zero = 0;
   for (;;) {
     const int b = wave_ticket(&counters[6]);
     if (b >= nb) break;
@@ -1076,7 +1090,67 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))
     V3 c = v3(0.0f, 0.0f, 0.0f);
     (void)batch_carries(cin, ndep, b, tag, true, c, ts);
     shade_batch(sc, cam, W, maxrec, dep_pix, ndep, b, c, out, zero);
+    if ((threadIdx.x & 63) == 0) atomicAdd(done_ctr, 1);
   }
+}
+
+__global__ void __launch_bounds__(kSideBlock) k_side(
+    Scene sc, Cam cam, int W, int H, int maxrec, const uint8_t* __restrict__ cls,
+    const long long* __restrict__ dep_pix, CinG* __restrict__ cin, int* __restrict__ counters,
+    int* __restrict__ batch_state, uint8_t* __restrict__ out,
+    unsigned long long* __restrict__ zcount, TeamState* __restrict__ ts, int resolve_blocks,
+    unsigned tag, int tiles) {
+  __shared__ int s_go;
+  // The grid is sized so that a resolver workgroup always fits beside k_side's workgroups on
+  // a CU (phase_c_side_blocks), so waiting here for every resolver workgroup to be resident
+  // cannot hold one out; the wait is bounded anyway (20 ms, then this workgroup leaves its
+  // work to k_finish).
+  if (threadIdx.x == 0) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    int go = 1;
+    while (__hip_atomic_load(&counters[5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+           resolve_blocks) {
+      if (__builtin_amdgcn_s_memrealtime() - t0 > 2000000ull) {
+        go = 0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(64);
+    }
+    s_go = go;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(&counters[s_go ? 12 : 13], 1);
+  if (!s_go) return;
+  int zero = 0;
+  const int ntiles = ((W + 7) >> 3) * ((H + 7) >> 3);
+  while (tiles) {   // the non-DEP pixels' colours (split shading only): always ready
+    const int t = wave_ticket(&counters[7]);
+    if (t >= ntiles) break;
+    shade_tile(sc, cam, W, H, maxrec, t, cls, out, zero);
+    if ((threadIdx.x & 63) == 0) atomicAdd(&counters[8], 1);
+  }
+  phase_c_passes(sc, cam, W, maxrec, dep_pix, cin, counters, batch_state, out, ts, tag, true,
+                 zero);
+  flush_events(zero, zcount);
+}
+
+// After the resolver: the tiles (when `tiles`) and DEP batches k_side has not claimed.
+__global__ void __launch_bounds__(kBlock) k_finish(
+    Scene sc, Cam cam, int W, int H, int maxrec, const uint8_t* __restrict__ cls,
+    const long long* __restrict__ dep_pix, CinG* __restrict__ cin, int* __restrict__ counters,
+    int* __restrict__ batch_state, uint8_t* __restrict__ out,
+    unsigned long long* __restrict__ zcount, TeamState* __restrict__ ts, unsigned tag,
+    int tiles) {
+  int zero = 0;
+  const int ntiles = ((W + 7) >> 3) * ((H + 7) >> 3);
+  while (tiles) {
+    const int t = wave_ticket(&counters[7]);
+    if (t >= ntiles) break;
+    shade_tile(sc, cam, W, H, maxrec, t, cls, out, zero);
+    if ((threadIdx.x & 63) == 0) atomicAdd(&counters[10], 1);
+  }
+  phase_c_passes(sc, cam, W, maxrec, dep_pix, cin, counters, batch_state, out, ts, tag, false,
+                 zero);
   flush_events(zero, zcount);
 }
 
@@ -1118,10 +1192,14 @@ hipError_t launch_parity(const LaunchScene& s, int W, int H, int maxrec, uint8_t
   const Cam cam = make_cam(s, W, H);
   const long long P = (long long)W * H;
   dim3 grid((W + kTile - 1) / kTile, (H + kTile - 1) / kTile);
-  hipLaunchKernelGGL(k_phase_a, grid, dim3(kBlock), 0, stream, sc, cam, W, H, maxrec, out,
-                     w.cls, w.wcarry, (DepRec*)w.deprec, zcount);
+  if (w.side && w.split_shade)   // carry part only; colours shaded beside the resolver (k_side)
+    hipLaunchKernelGGL(k_classify, grid, dim3(kBlock), 0, stream, sc, cam, W, H, maxrec, w.cls,
+                       w.wcarry, (DepRec*)w.deprec);
+  else
+    hipLaunchKernelGGL(k_phase_a, grid, dim3(kBlock), 0, stream, sc, cam, W, H, maxrec, out,
+                       w.cls, w.wcarry, (DepRec*)w.deprec, zcount);
   if (ev) (void)hipEventRecord(ev[0], stream);
-  (void)hipMemsetAsync(w.counters, 0, 8 * sizeof(int), stream);   // nseg, head, ndep, ...
+  (void)hipMemsetAsync(w.counters, 0, 16 * sizeof(int), stream);   // nseg, head, ndep, ...
   (void)hipMemsetAsync(w.team, 0, sizeof(TeamState), stream);     // error + round tags
   hipLaunchKernelGGL(k_row_stats, dim3(H), dim3(kScanBlock), 0, stream, w.cls, W, w.row_ndep,
                      w.row_lastw, w.row_lastdep);
@@ -1149,17 +1227,18 @@ hipError_t launch_parity(const LaunchScene& s, int W, int H, int maxrec, uint8_t
                      w.seg_order, w.counters, w.counters + 1, (CinG*)w.cin, w.team_blocks,
                      w.long_len, (TeamState*)w.team, w.trace, w.coop_group, w.wave_k,
                      w.resolve_k, w.epoch);
-  if (w.side) {   // phase C beside the resolver, on the CUs it leaves
+  if (w.side) {   // colours and phase C beside the resolver
     (void)hipStreamWaitEvent(w.side, w.fork, 0);
-    hipLaunchKernelGGL(k_phase_c_side, dim3(w.side_blocks), dim3(kSideBlock), kSideLds, w.side,
-                       sc, cam, W, maxrec, w.dep_pix, (CinG*)w.cin, w.counters, w.batch_state,
-                       out, zcount, (TeamState*)w.team, w.resolve_blocks, w.epoch);
+    hipLaunchKernelGGL(k_side, dim3(w.side_blocks), dim3(kSideBlock), w.side_lds, w.side, sc, cam,
+                       W, H, maxrec, w.cls, w.dep_pix, (CinG*)w.cin, w.counters, w.batch_state,
+                       out, zcount, (TeamState*)w.team, w.resolve_blocks, w.epoch,
+                       w.split_shade);
     (void)hipEventRecord(w.join, w.side);
   }
   if (ev) (void)hipEventRecord(ev[2], stream);
-  hipLaunchKernelGGL(k_phase_c, dim3(w.phase_c_blocks), dim3(kBlock), 0, stream, sc, cam, W,
-                     maxrec, w.dep_pix, (CinG*)w.cin, w.counters, w.batch_state, out, zcount,
-                     (TeamState*)w.team, w.epoch);
+  hipLaunchKernelGGL(k_finish, dim3(w.phase_c_blocks), dim3(kBlock), 0, stream, sc, cam, W, H,
+                     maxrec, w.cls, w.dep_pix, (CinG*)w.cin, w.counters, w.batch_state, out,
+                     zcount, (TeamState*)w.team, w.epoch, (w.side && w.split_shade) ? 1 : 0);
   if (w.side) (void)hipStreamWaitEvent(stream, w.join, 0);
   if (ev) (void)hipEventRecord(ev[3], stream);
   return hipGetLastError();
@@ -1167,14 +1246,36 @@ hipError_t launch_parity(const LaunchScene& s, int W, int H, int maxrec, uint8_t
 
 size_t team_state_bytes() { return sizeof(TeamState); }
 
-int phase_c_side_blocks(int cus) {
-  (void)hipFuncSetAttribute((const void*)k_phase_c_side,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, kSideLds);
+// k_side workgroups per CU such that one resolver workgroup (one wave per SIMD) still fits
+// beside them in every SIMD's 512 VGPRs: k_side waits for the resolver's census, so it must
+// never be what keeps a resolver workgroup out.
+// k_side's LDS reservation: more than a resolver workgroup leaves free on its CU (so k_side
+// only runs on CUs the resolver has left: sharing a CU with the carry chains and the team
+// measurably slows them), as small as that allows (more k_side workgroups per vacated CU).
+int side_lds_bytes(int resolve_dyn_lds) {
+  hipFuncAttributes a, b;
+  if (hipFuncGetAttributes(&a, (const void*)k_resolve<true>) != hipSuccess ||
+      hipFuncGetAttributes(&b, (const void*)k_resolve<false>) != hipSuccess)
+    return 65 * 1024;
+  const int lds_cu = 160 * 1024;
+  const int stat = (int)(a.sharedSizeBytes < b.sharedSizeBytes ? a.sharedSizeBytes
+                                                                : b.sharedSizeBytes);
+  int guard = lds_cu - resolve_dyn_lds - stat + 512;   // the most a resolver CU leaves free
+  guard = (guard + 511) / 512 * 512;
+  if (guard < 1024) guard = 1024;
+  return guard;
+}
+
+int phase_c_side_blocks(int cus, int side_lds) {
+  (void)hipFuncSetAttribute((const void*)k_side, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            side_lds);
   int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_phase_c_side, kSideBlock,
-                                                   kSideLds) != hipSuccess ||
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_side, kSideBlock, side_lds) !=
+          hipSuccess ||
       per_cu <= 0)
     per_cu = 1;
+  if (std::getenv("RC_SIDE_STATS"))
+    std::fprintf(stderr, "side lds %d -> %d workgroups per CU\n", side_lds, per_cu);
   return per_cu * cus;
 }
 

@@ -57,6 +57,21 @@ def test_configs(key, scenes, table):
     assert p3_md5(img) == table[key]["md5"], key
 
 
+@pytest.mark.parametrize("knob", ["RC_NO_SIDE", "RC_SPLIT_SHADE", "RC_RESOLVE_SHARED"])
+def test_parity_schedules(knob, scenes, table, monkeypatch):
+    """The parity pipeline's alternative schedules give the same bytes: phase C after the
+    resolver only (RC_NO_SIDE), colours shaded beside the resolver (RC_SPLIT_SHADE), and no
+    one-workgroup-per-CU reservation (RC_RESOLVE_SHARED, which also disables the side
+    stream)."""
+    monkeypatch.setenv(knob, "1")
+    for key in ("quadric:4096x4096:d6:parity", "reflection:2048x2048:d4:parity",
+                "quadric:333x517:d6:parity"):
+        scene, size, d, mode = key.split(":")
+        w, h = map(int, size.split("x"))
+        img = rc.render(scenes[scene], w, h, depth=int(d[1:]), mode=mode)
+        assert p3_md5(img) == table[key]["md5"], (knob, key)
+
+
 def test_c5_8192(scenes, table):
     """C5 image (quadric 8192x8192 d6) on one GPU, both modes."""
     for mode in ("parity", "fast"):
