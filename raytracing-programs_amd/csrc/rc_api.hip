@@ -75,7 +75,7 @@ struct DevCtx {
   DevBuf scene;        // uploaded packed scene
   const void* scene_src = nullptr;   // host image last uploaded
   // parity workspace
-  DevBuf cls, wcarry, deprec, rows, dep_pix, dep_key, dep_rec, seg_flag, blk_cnt, seg_start,
+  DevBuf cls, wcarry, deprec, rows, dep_pix, seg_key, seg_start,
       seg_order, batch_state,
       cin, counters, team, trace;
   int resident_blocks = 0;
@@ -192,10 +192,9 @@ int ensure_parity(DevCtx& c, int W, int H, rc::ParityWork& w) {
   const size_t P = (size_t)W * H;
   if (c.cls.ensure(P) || c.wcarry.ensure(P * sizeof(float4)) ||
       c.deprec.ensure(P * rc::deprec_bytes()) ||
-      c.rows.ensure((size_t)H * (2 * sizeof(int) + 4 * sizeof(long long)) + 256) ||
-      c.dep_pix.ensure(P * sizeof(long long)) || c.dep_key.ensure(P * sizeof(long long)) ||
-      c.dep_rec.ensure(P * rc::deprec_bytes()) || c.seg_flag.ensure(P) ||
-      c.blk_cnt.ensure((P / 1024 + 2) * sizeof(int)) ||
+      c.rows.ensure((size_t)H * (rc::row_stats_bytes() + 2 * sizeof(int) +
+                                 2 * sizeof(long long)) + 256) ||
+      c.dep_pix.ensure(P * sizeof(long long)) || c.seg_key.ensure(P * sizeof(long long)) ||
       c.seg_start.ensure(P * sizeof(int)) ||
       c.seg_order.ensure((size_t)rc::kSegOrderMax * sizeof(int)) ||
       c.batch_state.ensure((P / 64 + 2) * sizeof(int)) ||
@@ -222,17 +221,13 @@ int ensure_parity(DevCtx& c, int W, int H, rc::ParityWork& w) {
   w.cls = (uint8_t*)c.cls.p;
   w.wcarry = (float4*)c.wcarry.p;
   w.deprec = c.deprec.p;
-  w.row_lastw = (long long*)r;   r += (size_t)H * sizeof(long long);
-  w.row_lastdep = (long long*)r; r += (size_t)H * sizeof(long long);
   w.row_prevw = (long long*)r;   r += (size_t)H * sizeof(long long);
-  w.row_prevdep = (long long*)r; r += (size_t)H * sizeof(long long);
-  w.row_ndep = (int*)r;          r += (size_t)H * sizeof(int);
-  w.row_off = (int*)r;
+  w.row_prevd = (long long*)r;   r += (size_t)H * sizeof(long long);
+  w.row_stats = r;               r += (size_t)H * rc::row_stats_bytes();
+  w.row_off = (int*)r;           r += (size_t)H * sizeof(int);
+  w.row_soff = (int*)r;
   w.dep_pix = (long long*)c.dep_pix.p;
-  w.dep_key = (long long*)c.dep_key.p;
-  w.dep_rec = c.dep_rec.p;
-  w.seg_flag = (uint8_t*)c.seg_flag.p;
-  w.blk_cnt = (int*)c.blk_cnt.p;
+  w.seg_key = (long long*)c.seg_key.p;
   w.seg_start = (int*)c.seg_start.p;
   w.seg_order = (int*)c.seg_order.p;
   w.cin = c.cin.p;

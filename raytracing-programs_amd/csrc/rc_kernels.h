@@ -24,20 +24,16 @@ struct ParityWork {
   uint8_t* cls;             // [P]   pixel class (ident / writer / dep)
   float4* wcarry;           // [P]   writer carry-out
   void* deprec;             // [P]   DepRec (phase A -> B/C)
-  int* row_ndep;            // [H]
-  long long* row_lastw;     // [H]
-  long long* row_lastdep;   // [H]
-  int* row_off;             // [H]
-  long long* row_prevw;     // [H]
-  long long* row_prevdep;   // [H]
+  void* row_stats;          // [H]   RowStats (k_row_stats)
+  int* row_off;             // [H]   DEP offset of each row
+  int* row_soff;            // [H]   segment offset of each row
+  long long* row_prevw;     // [H]   last writer pixel before each row (-1: none)
+  long long* row_prevd;     // [H]   last DEP pixel before each row (-1: none)
   long long* dep_pix;       // [P]   DEP pixels in scan order
-  long long* dep_key;       // [P]   last writer before each DEP pixel (-1: none)
-  void* dep_rec;            // [P]   DepRec of each DEP entry, scan order
-  uint8_t* seg_flag;        // [P]   1 where a segment starts
-  int* blk_cnt;             // [P/1024] flag counts -> offsets
+  long long* seg_key;       // [P]   per segment: the writer pixel before it (-1: none)
   int* seg_start;           // [P]   segment starts, in scan order
   void* cin;                // [P]   resolved carry-in per DEP entry (CinG tagged granules)
-  int* counters;            // [8]   nseg, dequeue head, ndep, seg_order valid, tail cursor
+  int* counters;            // [16]  nseg, head, ndep, ordered, phase-C tickets, census, ...
   int* batch_state;         // [P/64+1] phase-C batch claim words (0 free, 1 claimed)
   hipStream_t side;         // phase C's side stream (null: phase C after the resolver only)
   hipEvent_t fork, join;    // side stream waits on fork; the main stream waits on join
@@ -71,6 +67,7 @@ hipError_t launch_parity(const LaunchScene& s, int W, int H, int maxrec, uint8_t
                          const hipEvent_t* ev);
 
 size_t deprec_bytes();
+size_t row_stats_bytes();
 size_t team_state_bytes();
 int resolve_blocks_resident(int cus, int lds_bytes);
 int side_lds_bytes(int resolve_dyn_lds);

@@ -9,8 +9,8 @@
 //   k_phase_a     the same plus the shading of every non-DEP pixel (used without the side
 //                 stream); with it, that shading runs in k_side beside the resolver.
 //   k_row_stats / k_row_scan / k_row_compact
-//                 scan-order compaction of the DEP pixels, each tagged with the last writer
-//                 before it (its segment key); segment starts appended to a work list.
+//                 scan-order list of the DEP pixels and the segment table (start, writer key),
+//                 one wave per row with ballot scans.
 //   k_resolve     parity phase B: exact carry chain.  One workgroup per segment (dequeued
 //                 from a counter): evaluate a window of DEP pixels at the current carry in
 //                 parallel, the first pixel that changes the carry ends the step.
@@ -117,247 +117,192 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_
 }
 
 // ------------------------------------------------------- scan-order DEP compaction --
-// Per row: number of DEP pixels, last writer index, last DEP index (global pixel ids).
-constexpr int kScanBlock = 256;
+// The DEP pixels in scan order (dep_pix, the resolver's and phase C's index), the segment
+// table (seg_start: first DEP index of every segment, seg_key: the writer pixel before it,
+// -1 = none) and the totals (counters[0] = segments, counters[2] = DEP pixels).  A segment
+// starts at a DEP pixel with no DEP pixel before it, or with a writer between it and the
+// previous DEP pixel.  One wave per row, ballot scans (no LDS, no barriers); the DEP records
+// stay where phase A wrote them (pixel-indexed) and the resolver gathers them by dep_pix.
+//   k_row_stats  per row: DEP count, segment starts decided inside the row, last writer,
+//                last DEP, the writer before the row's first DEP
+//   k_row_scan   one workgroup: exclusive scans over the rows (DEP offsets, last writer /
+//                last DEP before each row), the first DEP's start decision, segment offsets
+//   k_row_compact per row: dep_pix, seg_start, seg_key
+constexpr int kRowWaves = 4;   // rows per 256-thread workgroup
 
-__device__ __forceinline__ int block_sum(int v, int* sh) {
-  // 256 threads = 4 waves
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  const int w = threadIdx.x >> 6;
-  __syncthreads();
-  if ((threadIdx.x & 63) == 0) sh[w] = v;
-  __syncthreads();
-  int tot = 0;
-  for (int i = 0; i < (int)(blockDim.x >> 6); ++i) tot += sh[i];
-  return tot;
+__device__ __forceinline__ unsigned long long lanemask_lt() {
+  const int lane = threadIdx.x & 63;
+  return lane ? (~0ull >> (64 - lane)) : 0ull;
 }
-__device__ __forceinline__ long long block_max64(long long v, long long* sh) {
-  for (int o = 32; o > 0; o >>= 1) {
-    long long u = __shfl_xor(v, o, 64);
-    v = u > v ? u : v;
-  }
-  const int w = threadIdx.x >> 6;
-  __syncthreads();
-  if ((threadIdx.x & 63) == 0) sh[w] = v;
-  __syncthreads();
-  long long m = sh[0];
-  for (int i = 1; i < (int)(blockDim.x >> 6); ++i) m = sh[i] > m ? sh[i] : m;
-  return m;
-}
+__device__ __forceinline__ int hi_bit(unsigned long long m) { return 63 - __clzll((long long)m); }
 
-__global__ void __launch_bounds__(kScanBlock) k_row_stats(const uint8_t* __restrict__ cls, int W,
-                                                          int* __restrict__ row_ndep,
-                                                          long long* __restrict__ row_lastw,
-                                                          long long* __restrict__ row_lastdep) {
-  __shared__ int shi[16];
-  __shared__ long long shl[16];
-  const int y = blockIdx.x;
+struct RowStats {
+  int ndep, nstart;        // DEP pixels; segment starts other than the row's first DEP
+  long long lastw, lastd;  // last writer / DEP pixel of the row (-1: none)
+  long long wfirst;        // last writer before the row's first DEP pixel (-1: none)
+};
+
+__global__ void __launch_bounds__(256) k_row_stats(const uint8_t* __restrict__ cls, int W, int H,
+                                                   RowStats* __restrict__ rs) {
+  const int y = blockIdx.x * kRowWaves + (int)(threadIdx.x >> 6);
+  if (y >= H) return;
+  const int lane = threadIdx.x & 63;
   const long long base = (long long)y * W;
-  int nd = 0;
-  long long lw = -1, ld = -1;
-  for (int x = threadIdx.x; x < W; x += blockDim.x) {
-    const uint8_t c = cls[base + x];
-    if (c == kClsDep) {
-      nd++;
-      ld = base + x;
-    } else if (c == kClsWriter) {
-      lw = base + x;
-    }
-  }
-  nd = block_sum(nd, shi);
-  lw = block_max64(lw, shl);
-  ld = block_max64(ld, shl);
-  if (threadIdx.x == 0) {
-    row_ndep[y] = nd;
-    row_lastw[y] = lw;
-    row_lastdep[y] = ld;
-  }
-}
-
-// Single workgroup: exclusive scans over rows (sum of DEP counts, max of writer/DEP ids).
-__global__ void __launch_bounds__(1024) k_row_scan(int H, const int* __restrict__ row_ndep,
-                                                   const long long* __restrict__ row_lastw,
-                                                   const long long* __restrict__ row_lastdep,
-                                                   int* __restrict__ row_off,
-                                                   long long* __restrict__ row_prevw,
-                                                   long long* __restrict__ row_prevdep,
-                                                   int* __restrict__ ndep_total) {
-  __shared__ int s_cnt[1024];
-  __shared__ long long s_w[1024], s_d[1024];
-  // carried across chunks of 1024 rows
-  __shared__ int carry_cnt;
-  __shared__ long long carry_w, carry_d;
-  if (threadIdx.x == 0) {
-    carry_cnt = 0;
-    carry_w = -1;
-    carry_d = -1;
-  }
-  __syncthreads();
-  for (int base = 0; base < H; base += 1024) {
-    const int y = base + threadIdx.x;
-    s_cnt[threadIdx.x] = y < H ? row_ndep[y] : 0;
-    s_w[threadIdx.x] = y < H ? row_lastw[y] : -1;
-    s_d[threadIdx.x] = y < H ? row_lastdep[y] : -1;
-    __syncthreads();
-    // Hillis-Steele inclusive scan (1024 elements, 10 steps)
-    for (int o = 1; o < 1024; o <<= 1) {
-      int c = 0;
-      long long w = -1, d = -1;
-      if ((int)threadIdx.x >= o) {
-        c = s_cnt[threadIdx.x - o];
-        w = s_w[threadIdx.x - o];
-        d = s_d[threadIdx.x - o];
-      }
-      __syncthreads();
-      s_cnt[threadIdx.x] += c;
-      if (w > s_w[threadIdx.x]) s_w[threadIdx.x] = w;
-      if (d > s_d[threadIdx.x]) s_d[threadIdx.x] = d;
-      __syncthreads();
-    }
-    if (y < H) {
-      const int exc = (threadIdx.x ? s_cnt[threadIdx.x - 1] : 0);
-      const long long pw = threadIdx.x ? s_w[threadIdx.x - 1] : -1;
-      const long long pd = threadIdx.x ? s_d[threadIdx.x - 1] : -1;
-      row_off[y] = carry_cnt + exc;
-      row_prevw[y] = pw > carry_w ? pw : carry_w;
-      row_prevdep[y] = pd > carry_d ? pd : carry_d;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      carry_cnt += s_cnt[1023];
-      if (s_w[1023] > carry_w) carry_w = s_w[1023];
-      if (s_d[1023] > carry_d) carry_d = s_d[1023];
-    }
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) *ndep_total = carry_cnt;
-}
-
-// Per row: write the DEP pixels in scan order (compact DepRec + pixel id), their segment key
-// (last writer before the pixel, -1 = none: carry (0,0,0)) and a segment-start flag.
-__global__ void __launch_bounds__(kScanBlock) k_row_compact(
-    const uint8_t* __restrict__ cls, int W, const int* __restrict__ row_off,
-    const long long* __restrict__ row_prevw, const long long* __restrict__ row_prevdep,
-    const DepRec* __restrict__ deprec, DepRec* __restrict__ dep_rec,
-    long long* __restrict__ dep_pix, long long* __restrict__ dep_key,
-    uint8_t* __restrict__ seg_flag) {
-  __shared__ int s_cnt[kScanBlock];
-  __shared__ long long s_w[kScanBlock], s_d[kScanBlock];
-  __shared__ int c_cnt;
-  __shared__ long long c_w, c_d;
-  const int y = blockIdx.x;
-  const long long base = (long long)y * W;
-  if (threadIdx.x == 0) {
-    c_cnt = row_off[y];
-    c_w = row_prevw[y];
-    c_d = row_prevdep[y];
-  }
-  __syncthreads();
-  for (int x0 = 0; x0 < W; x0 += kScanBlock) {
-    const int x = x0 + threadIdx.x;
+  const unsigned long long lt = lanemask_lt();
+  int nd = 0, ns = 0;
+  long long lw = -1, ld = -1, wf = -1;
+  for (int x0 = 0; x0 < W; x0 += 64) {
+    const int x = x0 + lane;
     const uint8_t c = x < W ? cls[base + x] : kClsIdent;
-    const long long pix = base + x;
-    s_cnt[threadIdx.x] = (c == kClsDep);
-    s_w[threadIdx.x] = (c == kClsWriter) ? pix : -1;
-    s_d[threadIdx.x] = (c == kClsDep) ? pix : -1;
-    __syncthreads();
-    for (int o = 1; o < kScanBlock; o <<= 1) {
-      int cc = 0;
-      long long w = -1, d = -1;
-      if ((int)threadIdx.x >= o) {
-        cc = s_cnt[threadIdx.x - o];
-        w = s_w[threadIdx.x - o];
-        d = s_d[threadIdx.x - o];
+    const unsigned long long md = __ballot(c == kClsDep), mw = __ballot(c == kClsWriter);
+    // a DEP lane (not the row's first DEP) starts a segment when a writer lies between it
+    // and the previous DEP: last writer before it > previous DEP before it
+    long long kw = (mw & lt) ? base + x0 + hi_bit(mw & lt) : lw;
+    long long pd = (md & lt) ? base + x0 + hi_bit(md & lt) : ld;
+    const bool st = c == kClsDep && pd >= 0 && kw > pd;
+    ns += __popcll(__ballot(st));
+    if (wf < 0 && ld < 0 && md) {   // first DEP of the row is in this chunk
+      const int f = __ffsll((long long)md) - 1;
+      const unsigned long long wb = mw & ((f ? (~0ull >> (64 - f)) : 0ull));
+      wf = wb ? base + x0 + hi_bit(wb) : lw;
+    }
+    nd += __popcll(md);
+    if (mw) lw = base + x0 + hi_bit(mw);
+    if (md) ld = base + x0 + hi_bit(md);
+  }
+  if (lane == 0) rs[y] = RowStats{nd, ns, lw, ld, wf};
+}
+
+// One workgroup of 1024: chunks of 1024 rows, wave-level inclusive scans + a carry.
+__global__ void __launch_bounds__(1024) k_row_scan(int H, const RowStats* __restrict__ rs,
+                                                   int* __restrict__ row_off,
+                                                   int* __restrict__ row_soff,
+                                                   long long* __restrict__ row_prevw,
+                                                   long long* __restrict__ row_prevd,
+                                                   int* __restrict__ counters) {
+  __shared__ int w_cnt[16], w_seg[16];
+  __shared__ long long w_w[16], w_d[16];
+  __shared__ int c_cnt, c_seg;
+  __shared__ long long c_w, c_d;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (threadIdx.x == 0) {
+    c_cnt = 0;
+    c_seg = 0;
+    c_w = -1;
+    c_d = -1;
+  }
+  __syncthreads();
+  for (int y0 = 0; y0 < H; y0 += 1024) {
+    const int y = y0 + threadIdx.x;
+    RowStats r = y < H ? rs[y] : RowStats{0, 0, -1, -1, -1};
+    // inclusive wave scans: count (sum), last writer / DEP (max)
+    int cnt = r.ndep;
+    long long lw = r.lastw, ld = r.lastd;
+    for (int o = 1; o < 64; o <<= 1) {
+      const int c2 = __shfl_up(cnt, o, 64);
+      const long long w2 = __shfl_up(lw, o, 64), d2 = __shfl_up(ld, o, 64);
+      if (lane >= o) {
+        cnt += c2;
+        lw = w2 > lw ? w2 : lw;
+        ld = d2 > ld ? d2 : ld;
       }
-      __syncthreads();
-      s_cnt[threadIdx.x] += cc;
-      if (w > s_w[threadIdx.x]) s_w[threadIdx.x] = w;
-      if (d > s_d[threadIdx.x]) s_d[threadIdx.x] = d;
-      __syncthreads();
     }
-    if (c == kClsDep) {
-      const int idx = c_cnt + s_cnt[threadIdx.x] - 1;
-      // writers strictly before this pixel: inclusive scan includes none at this position
-      // (a DEP pixel is not a writer), so the inclusive max is the exclusive one.
-      long long key = s_w[threadIdx.x];
-      if (c_w > key) key = c_w;
-      long long prevd = threadIdx.x ? s_d[threadIdx.x - 1] : -1;
-      if (c_d > prevd) prevd = c_d;
-      dep_pix[idx] = pix;
-      dep_key[idx] = key;
-      dep_rec[idx] = deprec[pix];
-      seg_flag[idx] = (prevd < 0 || key > prevd) ? 1 : 0;
+    if (lane == 63) {
+      w_cnt[wave] = cnt;
+      w_w[wave] = lw;
+      w_d[wave] = ld;
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-      c_cnt += s_cnt[kScanBlock - 1];
-      if (s_w[kScanBlock - 1] > c_w) c_w = s_w[kScanBlock - 1];
-      if (s_d[kScanBlock - 1] > c_d) c_d = s_d[kScanBlock - 1];
+    int pc = c_cnt;
+    long long pw = c_w, pdd = c_d;
+    for (int q = 0; q < wave; ++q) {
+      pc += w_cnt[q];
+      pw = w_w[q] > pw ? w_w[q] : pw;
+      pdd = w_d[q] > pdd ? w_d[q] : pdd;
+    }
+    // exclusive values for this row
+    const int exc_cnt = pc + cnt - r.ndep;
+    long long exw = __shfl_up(lw, 1, 64), exd = __shfl_up(ld, 1, 64);
+    if (lane == 0) {
+      exw = -1;
+      exd = -1;
+    }
+    exw = exw > pw ? exw : pw;
+    exd = exd > pdd ? exd : pdd;
+    // the row's first DEP: its writer key and the DEP before it decide whether it starts one
+    int nseg = r.nstart;
+    if (r.ndep > 0) {
+      const long long key = r.wfirst > exw ? r.wfirst : exw;
+      if (exd < 0 || key > exd) nseg += 1;
+    }
+    // segment offsets: a second scan (sum)
+    int sc = nseg;
+    for (int o = 1; o < 64; o <<= 1) {
+      const int s2 = __shfl_up(sc, o, 64);
+      if (lane >= o) sc += s2;
+    }
+    if (lane == 63) w_seg[wave] = sc;
+    __syncthreads();
+    int ps = c_seg;
+    for (int q = 0; q < wave; ++q) ps += w_seg[q];
+    if (y < H) {
+      row_off[y] = exc_cnt;
+      row_soff[y] = ps + sc - nseg;
+      row_prevw[y] = exw;
+      row_prevd[y] = exd;
+    }
+    __syncthreads();
+    if (threadIdx.x == 1023) {
+      c_cnt = pc + cnt;
+      c_seg = ps + sc;
+      c_w = lw > pw ? lw : pw;
+      c_d = ld > pdd ? ld : pdd;
     }
     __syncthreads();
   }
+  if (threadIdx.x == 0) {
+    counters[0] = c_seg;
+    counters[2] = c_cnt;
+  }
 }
 
-// Ordered segment table: flag count per 1024 entries -> one-block scan -> scatter.
-constexpr int kFlagBlock = 1024;
-
-__global__ void __launch_bounds__(kFlagBlock) k_flag_count(const uint8_t* __restrict__ flag,
-                                                           const int* __restrict__ ndep_p,
-                                                           int* __restrict__ blk_cnt) {
-  __shared__ int sh[16];
-  const int ndep = *ndep_p;
-  const long long i = (long long)blockIdx.x * kFlagBlock + threadIdx.x;
-  if ((long long)blockIdx.x * kFlagBlock >= ndep) return;
-  int v = (i < ndep) ? flag[i] : 0;
-  v = block_sum(v, sh);
-  if (threadIdx.x == 0) blk_cnt[blockIdx.x] = v;
-}
-
-__global__ void __launch_bounds__(1024) k_flag_scan(const int* __restrict__ ndep_p,
-                                                    int* __restrict__ blk_cnt,
-                                                    int* __restrict__ nseg_p) {
-  __shared__ int s[1024];
-  __shared__ int carry;
-  const int nblk = (*ndep_p + kFlagBlock - 1) / kFlagBlock;
-  if (threadIdx.x == 0) carry = 0;
-  __syncthreads();
-  for (int b0 = 0; b0 < nblk; b0 += 1024) {
-    const int b = b0 + threadIdx.x;
-    const int v = b < nblk ? blk_cnt[b] : 0;
-    s[threadIdx.x] = v;
-    __syncthreads();
-    for (int o = 1; o < 1024; o <<= 1) {
-      const int u = (int)threadIdx.x >= o ? s[threadIdx.x - o] : 0;
-      __syncthreads();
-      s[threadIdx.x] += u;
-      __syncthreads();
+__global__ void __launch_bounds__(256) k_row_compact(
+    const uint8_t* __restrict__ cls, int W, int H, const int* __restrict__ row_off,
+    const int* __restrict__ row_soff, const long long* __restrict__ row_prevw,
+    const long long* __restrict__ row_prevd, long long* __restrict__ dep_pix,
+    int* __restrict__ seg_start, long long* __restrict__ seg_key) {
+  const int y = blockIdx.x * kRowWaves + (int)(threadIdx.x >> 6);
+  if (y >= H) return;
+  const int lane = threadIdx.x & 63;
+  const long long base = (long long)y * W;
+  const unsigned long long lt = lanemask_lt();
+  int idx0 = row_off[y], s0 = row_soff[y];
+  long long lw = row_prevw[y], ld = row_prevd[y];
+  for (int x0 = 0; x0 < W; x0 += 64) {
+    const int x = x0 + lane;
+    const uint8_t c = x < W ? cls[base + x] : kClsIdent;
+    const unsigned long long md = __ballot(c == kClsDep), mw = __ballot(c == kClsWriter);
+    if (md) {
+      const long long kw = (mw & lt) ? base + x0 + hi_bit(mw & lt) : lw;
+      const long long pd = (md & lt) ? base + x0 + hi_bit(md & lt) : ld;
+      const bool dep = c == kClsDep;
+      const bool st = dep && (pd < 0 || kw > pd);
+      const unsigned long long ms = __ballot(st);
+      if (dep) {
+        const int idx = idx0 + __popcll(md & lt);
+        dep_pix[idx] = base + x;
+        if (st) {
+          const int si = s0 + __popcll(ms & lt);
+          seg_start[si] = idx;
+          seg_key[si] = kw;
+        }
+      }
+      idx0 += __popcll(md);
+      s0 += __popcll(ms);
+      ld = base + x0 + hi_bit(md);
     }
-    if (b < nblk) blk_cnt[b] = carry + s[threadIdx.x] - v;   // exclusive offset
-    __syncthreads();
-    if (threadIdx.x == 0) carry += s[1023];
-    __syncthreads();
+    if (mw) lw = base + x0 + hi_bit(mw);
   }
-  if (threadIdx.x == 0) *nseg_p = carry;
-}
-
-__global__ void __launch_bounds__(kFlagBlock) k_flag_scatter(const uint8_t* __restrict__ flag,
-                                                             const int* __restrict__ ndep_p,
-                                                             const int* __restrict__ blk_off,
-                                                             int* __restrict__ seg_start) {
-  __shared__ int s[kFlagBlock];
-  const int ndep = *ndep_p;
-  if ((long long)blockIdx.x * kFlagBlock >= ndep) return;
-  const long long i = (long long)blockIdx.x * kFlagBlock + threadIdx.x;
-  const int v = (i < ndep) ? flag[i] : 0;
-  s[threadIdx.x] = v;
-  __syncthreads();
-  for (int o = 1; o < kFlagBlock; o <<= 1) {
-    const int u = (int)threadIdx.x >= o ? s[threadIdx.x - o] : 0;
-    __syncthreads();
-    s[threadIdx.x] += u;
-    __syncthreads();
-  }
-  if (v) seg_start[blk_off[blockIdx.x] + s[threadIdx.x] - 1] = (int)i;
 }
 
 // ------------------------------------------------------------ parity phase B: carry --
@@ -381,12 +326,18 @@ __device__ __forceinline__ bool same_bits(V3 a, V3 b) {
          __float_as_uint(a.z) == __float_as_uint(b.z);
 }
 
-__device__ __forceinline__ V3 seg_init_carry(const long long* __restrict__ dep_key,
-                                             const float4* __restrict__ wcarry, int start) {
-  const long long key = dep_key[start];
+__device__ __forceinline__ V3 seg_init_carry(const long long* __restrict__ seg_key,
+                                             const float4* __restrict__ wcarry, int s) {
+  const long long key = seg_key[s];
   if (key < 0) return v3(0.0f, 0.0f, 0.0f);
   const float4 k4 = wcarry[key];
   return v3(k4.x, k4.y, k4.z);
+}
+
+// DEP entry j's record: phase A wrote it at the pixel (dep_pix[j]); gathered, never copied.
+__device__ __forceinline__ DepRec rec_at(const DepRec* __restrict__ deprec,
+                                         const long long* __restrict__ dep_pix, int j) {
+  return deprec[dep_pix[j]];
 }
 
 // Resolve the 64 entries [base, base+64) ∩ [.., end) of one wave at carry `c`, changers
@@ -423,7 +374,8 @@ struct WinStats {
 };
 
 __device__ __forceinline__ int wave_window(const Scene& sc, int maxrec,
-                                           const DepRec* __restrict__ dep_rec, int base,
+                                           const DepRec* __restrict__ deprec,
+                                           const long long* __restrict__ dep_pix, int base,
                                            int end, V3& c, V3& mine, const LaneShape& ls,
                                            int G, bool& dense, bool& changed,
                                            WinStats& ws, int K
@@ -436,7 +388,7 @@ __device__ __forceinline__ int wave_window(const Scene& sc, int maxrec,
   const int nvalid = end - base < 64 ? end - base : 64;
   const bool valid = lane < nvalid;
   DepRec r;
-  if (valid) r = dep_rec[idx];
+  if (valid) r = rec_at(deprec, dep_pix, idx);
   mine = c;
   changed = false;
   int zero = 0;
@@ -749,8 +701,9 @@ __device__ __forceinline__ bool team_collect(TeamState* ts, int round, int b, un
 
 template <bool kLds>
 __global__ void __launch_bounds__(kResolveBlock) k_resolve(
-    Scene sc, int maxrec, const DepRec* __restrict__ dep_rec,
-    const long long* __restrict__ dep_key, const float4* __restrict__ wcarry,
+    Scene sc, int maxrec, const DepRec* __restrict__ deprec,
+    const long long* __restrict__ dep_pix, const long long* __restrict__ seg_key,
+    const float4* __restrict__ wcarry,
     const int* __restrict__ seg_start, const int* __restrict__ seg_order,
     int* __restrict__ counters, int* __restrict__ head,
     CinG* __restrict__ cin, int team_blocks, int long_len, TeamState* __restrict__ ts,
@@ -811,7 +764,7 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
       const unsigned long long t_seg = __builtin_amdgcn_s_memrealtime();
       const unsigned long long c_seg = __builtin_amdgcn_s_memtime();
       int rounds_here = 0;
-      V3 c = seg_init_carry(dep_key, wcarry, start);
+      V3 c = seg_init_carry(seg_key, wcarry, s);
       int j = start;
       bool resolve = false;
       while (j < end) {
@@ -829,7 +782,7 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
           V3 o = c;
           if (valid) {
             int zero = 0;
-            o = carry_path(sc, dep_rec[idx], maxrec, c, zero);
+            o = carry_path(sc, rec_at(deprec, dep_pix, idx), maxrec, c, zero);
           }
           const unsigned long long m = __ballot(valid && !same_bits(o, c));
           const int k = m ? __ffsll((long long)m) - 1 : -1;
@@ -887,13 +840,13 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
             bool dense = true;   // the cluster starts right after a changer
             // records of the first window; later windows are prefetched one ahead
             const int t = threadIdx.x;
-            if (j + t < end) s_bw.rec[t] = dep_rec[j + t];
+            if (j + t < end) s_bw.rec[t] = rec_at(deprec, dep_pix, j + t);
             __syncthreads();
             while (j < end) {
               const int nv = end - j < kResolveBlock ? end - j : kResolveBlock;
               DepRec nxt;
               const int jn = j + nv;
-              if (jn + t < end) nxt = dep_rec[jn + t];
+              if (jn + t < end) nxt = rec_at(deprec, dep_pix, jn + t);
               bool changed;
               block_window(sc, maxrec, s_bw, j, nv, c, ls, G, dense, changed, resolve_k, cin,
                            tag, tws);
@@ -956,13 +909,13 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
     const unsigned long long t_seg = __builtin_amdgcn_s_memrealtime();
     const unsigned long long c_seg = __builtin_amdgcn_s_memtime();
     int iters = 0;
-    V3 c = seg_init_carry(dep_key, wcarry, start);
+    V3 c = seg_init_carry(seg_key, wcarry, s);
     bool dense = false;
     WinStats ws = {0, 0, 0};
     for (int j = start; j < end; j += 64) {
       V3 mine;
       bool changed;
-      iters += wave_window(sc, maxrec, dep_rec, j, end, c, mine, ls, G, dense, changed, ws,
+      iters += wave_window(sc, maxrec, deprec, dep_pix, j, end, c, mine, ls, G, dense, changed, ws,
                            wave_k
 #if RC_STAMPS
                            , &stp
@@ -1190,7 +1143,6 @@ hipError_t launch_parity(const LaunchScene& s, int W, int H, int maxrec, uint8_t
   // [3] after phase C
   const Scene sc = make_scene(s);
   const Cam cam = make_cam(s, W, H);
-  const long long P = (long long)W * H;
   dim3 grid((W + kTile - 1) / kTile, (H + kTile - 1) / kTile);
   if (w.side && w.split_shade)   // carry part only; colours shaded beside the resolver (k_side)
     hipLaunchKernelGGL(k_classify, grid, dim3(kBlock), 0, stream, sc, cam, W, H, maxrec, w.cls,
@@ -1201,20 +1153,14 @@ hipError_t launch_parity(const LaunchScene& s, int W, int H, int maxrec, uint8_t
   if (ev) (void)hipEventRecord(ev[0], stream);
   (void)hipMemsetAsync(w.counters, 0, 16 * sizeof(int), stream);   // nseg, head, ndep, ...
   (void)hipMemsetAsync(w.team, 0, sizeof(TeamState), stream);     // error + round tags
-  hipLaunchKernelGGL(k_row_stats, dim3(H), dim3(kScanBlock), 0, stream, w.cls, W, w.row_ndep,
-                     w.row_lastw, w.row_lastdep);
-  hipLaunchKernelGGL(k_row_scan, dim3(1), dim3(1024), 0, stream, H, w.row_ndep, w.row_lastw,
-                     w.row_lastdep, w.row_off, w.row_prevw, w.row_prevdep, w.counters + 2);
-  hipLaunchKernelGGL(k_row_compact, dim3(H), dim3(kScanBlock), 0, stream, w.cls, W, w.row_off,
-                     w.row_prevw, w.row_prevdep, (const DepRec*)w.deprec, (DepRec*)w.dep_rec,
-                     w.dep_pix, w.dep_key, w.seg_flag);
-  const int nblk = (int)((P + kFlagBlock - 1) / kFlagBlock);
-  hipLaunchKernelGGL(k_flag_count, dim3(nblk), dim3(kFlagBlock), 0, stream, w.seg_flag,
-                     w.counters + 2, w.blk_cnt);
-  hipLaunchKernelGGL(k_flag_scan, dim3(1), dim3(1024), 0, stream, w.counters + 2, w.blk_cnt,
-                     w.counters + 0);
-  hipLaunchKernelGGL(k_flag_scatter, dim3(nblk), dim3(kFlagBlock), 0, stream, w.seg_flag,
-                     w.counters + 2, w.blk_cnt, w.seg_start);
+  const int row_blocks = (H + kRowWaves - 1) / kRowWaves;
+  hipLaunchKernelGGL(k_row_stats, dim3(row_blocks), dim3(256), 0, stream, w.cls, W, H,
+                     (RowStats*)w.row_stats);
+  hipLaunchKernelGGL(k_row_scan, dim3(1), dim3(1024), 0, stream, H, (const RowStats*)w.row_stats,
+                     w.row_off, w.row_soff, w.row_prevw, w.row_prevd, w.counters);
+  hipLaunchKernelGGL(k_row_compact, dim3(row_blocks), dim3(256), 0, stream, w.cls, W, H,
+                     w.row_off, w.row_soff, w.row_prevw, w.row_prevd, w.dep_pix, w.seg_start,
+                     w.seg_key);
   hipLaunchKernelGGL(k_seg_order, dim3(1), dim3(1024), 0, stream, w.seg_start, w.counters,
                      w.seg_order, w.batch_state);
   // resolve_lds > 80 KiB keeps one resolver block (4 waves, one per SIMD) per CU: the chain
@@ -1223,8 +1169,8 @@ hipError_t launch_parity(const LaunchScene& s, int W, int H, int maxrec, uint8_t
   if (w.side) (void)hipEventRecord(w.fork, stream);
   auto kres = s.n <= kLdsShapes ? k_resolve<true> : k_resolve<false>;
   hipLaunchKernelGGL(kres, dim3(w.resolve_blocks), dim3(kResolveBlock), w.resolve_lds, stream, sc,
-                     maxrec, (const DepRec*)w.dep_rec, w.dep_key, w.wcarry, w.seg_start,
-                     w.seg_order, w.counters, w.counters + 1, (CinG*)w.cin, w.team_blocks,
+                     maxrec, (const DepRec*)w.deprec, w.dep_pix, w.seg_key, w.wcarry,
+                     w.seg_start, w.seg_order, w.counters, w.counters + 1, (CinG*)w.cin, w.team_blocks,
                      w.long_len, (TeamState*)w.team, w.trace, w.coop_group, w.wave_k,
                      w.resolve_k, w.epoch);
   if (w.side) {   // colours and phase C beside the resolver
@@ -1295,5 +1241,6 @@ int resolve_blocks_resident(int cus, int lds_bytes) {
 }
 
 size_t deprec_bytes() { return sizeof(DepRec); }
+size_t row_stats_bytes() { return sizeof(RowStats); }
 
 }  // namespace rc
