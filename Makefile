@@ -45,7 +45,7 @@ $(LIB)/libraycast_hip.so: $(OBJ)/rc_kernels.o $(OBJ)/rc_api.o $(OBJ)/rc_scene.o
 
 $(LIB)/libraycast_front.so: $(FRONT_SRC) include/raycast_hip.h
 	@mkdir -p $(LIB)
-	$(CC) $(CFLAGS) -shared $(FRONT_SRC) -o $@ -lm
+	$(CC) $(CFLAGS) -shared $(FRONT_SRC) -o $@ -lm -lpthread
 
 $(BIN)/raytrace: $(SRC)/front/raytrace_main.c $(LIB)/libraycast_front.so $(LIB)/libraycast_hip.so
 	@mkdir -p $(BIN)
