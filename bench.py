@@ -70,6 +70,24 @@ def pmc_traffic(kernel, scene, size, depth, mode):
     return None, None
 
 
+def end_to_end(pkg, scene, W, H, depth, mode, reps=5):
+    """The drop-in path's rate: rc_render() into a host pixmap — scene
+    upload, every kernel and the device-to-host copy into pageable memory, as raycast()
+    runs it.  Reported beside `value` (device-resident), never as it."""
+    import time as _t
+    pkg.render(scene, W, H, depth=depth, mode=mode)   # warm: host buffers, scene upload
+    ts = []
+    for _ in range(reps):
+        t0 = _t.perf_counter()
+        pkg.render(scene, W, H, depth=depth, mode=mode)
+        ts.append(_t.perf_counter() - t0)
+    ts.sort()
+    med = ts[len(ts) // 2]
+    return {"value": round(W * H / med, 1), "unit": "rays/s", "ms": round(med * 1e3, 3),
+            "note": "rc_render into a pageable host pixmap (upload + kernels + D2H), median of "
+                    f"{reps}"}
+
+
 def cpu_baseline(scene_path, size, depth):
     """The reference itself (oracle/_ref/ref_timer_d<depth>: the C/ sources built like
     C/Makefile:4, raycast() timed alone) on the same image on one pinned host core; falls
@@ -231,6 +249,8 @@ def main():
                              if phases["total_ms"] else None,
                              "peak": PEAK_HBM_GBS, "unit": "GB/s"},
         }
+        if world == 1 and not sharded:
+            line["end_to_end"] = end_to_end(pkg, scene, W, H, args.depth, mode)
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(scene_path, args.size, args.depth)
         print(json.dumps(line), flush=True)
