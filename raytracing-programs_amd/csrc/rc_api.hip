@@ -182,9 +182,12 @@ int upload_scene(DevCtx& c, const rc_scene* s, rc::LaunchScene& ls) {
   ls.cam_w = h->cam_w;
   ls.cam_h = h->cam_h;
   ls.refl_mask = 0;
+  ls.has_quadric = 0;
   const rc_shape* hs = (const rc_shape*)((const char*)h + h->off_shapes);
   for (int k = 0; k < h->n && k < 64; ++k)
     if (hs[k].refl > 0.0f) ls.refl_mask |= 1ull << k;
+  for (int k = 0; k < h->n; ++k)
+    if (hs[k].type == RC_SHAPE_QUADRIC) ls.has_quadric = 1;
   return 0;
 }
 

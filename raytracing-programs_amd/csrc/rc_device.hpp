@@ -38,6 +38,7 @@ struct Scene {
   const rc_shade_pair* __restrict__ pairs;
   int n, m;
   unsigned long long refl_mask;          // bit k: shape k has reflectivity > 0 (k < 64)
+  int has_quadric;                       // any quadric: picks the evaluator specialisation
 };
 
 // refl[obj] > 0 (C/raycast.c:352) from a register bitmask when n <= 64
@@ -685,63 +686,69 @@ __device__ __forceinline__ unsigned long long stamp_now() {
 // The plane's f32 quotient (-num)/den is taken as (float)((double)(-num) / (double)den):
 // double rounding is innocuous for division when 53 >= 2*24 + 2.
 
-// normalize() without the branch (the zero-length case keeps the input, not counted: only
-// the final shading pass counts events).
-// test_shape() for any type, branch-free.
+// test_shape() for any type, branch-free.  kQuad = false: the scene has no quadric, so the
+// quadric part is compiled out (every quadric term below is dead).
+template <bool kQuad>
 __device__ __forceinline__ bool test_unified(const rc_shape& s, V3 O, V3 D, RayK rk, int skip,
                                              float& t) {
   const int type = s.type;
   const bool isS = type == RC_SHAPE_SPHERE, isP = type == RC_SHAPE_PLANE,
-             isQ = type == RC_SHAPE_QUADRIC;
+             isQ = kQuad && type == RC_SHAPE_QUADRIC;
   // origin-only parts (sphere c, plane num, quadric cq)
   const V3 tv = v3(O.x - s.p[0], O.y - s.p[1], O.z - s.p[2]);
   const float cS = (float)((double)dot(tv, tv) - s.r2);
   const float numP = pin(dot(tv, v3(s.n[0], s.n[1], s.n[2])));
-  double acc;
-  acc = s.A * ((double)O.x * (double)O.x);
-  acc = acc + s.B * ((double)O.y * (double)O.y);
-  acc = acc + s.C * ((double)O.z * (double)O.z);
-  acc = acc + (double)(s.qd * O.x * O.y);
-  acc = acc + (double)(s.qe * O.x * O.z);
-  acc = acc + (double)(s.qf * O.y * O.z);
-  acc = acc + (double)(s.qg * O.x);
-  acc = acc + (double)(s.qh * O.y);
-  acc = acc + (double)(s.qi * O.z);
-  acc = acc + (double)s.qj;
-  const float cq = (float)acc;
-  // direction parts
+  // direction parts (sphere b and disc, plane den)
   const float bS = 2.0f * dot(D, tv);
   const float facS = rk.a4 * cS;
   const float discS = (float)((double)bS * (double)bS - (double)facS);
   const float denP = dot(D, v3(s.n[0], s.n[1], s.n[2]));
-  acc = s.A * ((double)D.x * (double)D.x);
-  acc = acc + s.B * ((double)D.y * (double)D.y);
-  acc = acc + s.C * ((double)D.z * (double)D.z);
-  acc = acc + (double)(s.qd * D.x * D.y);
-  acc = acc + (double)(s.qe * D.x * D.z);
-  acc = acc + (double)(s.qf * D.y * D.z);
-  const float aq = (float)acc;
-  acc = 2.0 * s.A * (double)O.x * (double)D.x;
-  acc = acc + 2.0 * s.B * (double)O.y * (double)D.y;
-  acc = acc + 2.0 * s.C * (double)O.z * (double)D.z;
-  acc = acc + (double)(s.qd * (O.x * D.y + O.y * D.x));
-  acc = acc + (double)(s.qe * (O.x * D.z + O.z * D.x));
-  acc = acc + (double)(s.qf * (O.y * D.z + O.z * D.y));
-  acc = acc + (double)(s.qg * D.x);
-  acc = acc + (double)(s.qh * D.y);
-  acc = acc + (double)(s.qi * D.z);
-  const float bq = (float)acc;
-  const float discQ = (float)((double)bq * (double)bq - 4.0 * (double)aq * (double)cq);
-  const bool lin = (double)aq == 0.0;
+  float cq = 0.0f, aq = 0.0f, bq = 0.0f, discQ = 0.0f;
+  bool lin = false;
+  if constexpr (kQuad) {
+    double acc;
+    acc = s.A * ((double)O.x * (double)O.x);
+    acc = acc + s.B * ((double)O.y * (double)O.y);
+    acc = acc + s.C * ((double)O.z * (double)O.z);
+    acc = acc + (double)(s.qd * O.x * O.y);
+    acc = acc + (double)(s.qe * O.x * O.z);
+    acc = acc + (double)(s.qf * O.y * O.z);
+    acc = acc + (double)(s.qg * O.x);
+    acc = acc + (double)(s.qh * O.y);
+    acc = acc + (double)(s.qi * O.z);
+    acc = acc + (double)s.qj;
+    cq = (float)acc;
+    acc = s.A * ((double)D.x * (double)D.x);
+    acc = acc + s.B * ((double)D.y * (double)D.y);
+    acc = acc + s.C * ((double)D.z * (double)D.z);
+    acc = acc + (double)(s.qd * D.x * D.y);
+    acc = acc + (double)(s.qe * D.x * D.z);
+    acc = acc + (double)(s.qf * D.y * D.z);
+    aq = (float)acc;
+    acc = 2.0 * s.A * (double)O.x * (double)D.x;
+    acc = acc + 2.0 * s.B * (double)O.y * (double)D.y;
+    acc = acc + 2.0 * s.C * (double)O.z * (double)D.z;
+    acc = acc + (double)(s.qd * (O.x * D.y + O.y * D.x));
+    acc = acc + (double)(s.qe * (O.x * D.z + O.z * D.x));
+    acc = acc + (double)(s.qf * (O.y * D.z + O.z * D.y));
+    acc = acc + (double)(s.qg * D.x);
+    acc = acc + (double)(s.qh * D.y);
+    acc = acc + (double)(s.qi * D.z);
+    bq = (float)acc;
+    discQ = (float)((double)bq * (double)bq - 4.0 * (double)aq * (double)cq);
+    lin = (double)aq == 0.0;
+  }
   // shared tail: one sqrt, two quotients
-  const float B = isS ? bS : bq;
-  const float disc = isS ? discS : discQ;
+  const float B = kQuad ? (isS ? bS : bq) : bS;
+  const float disc = kQuad ? (isS ? discS : discQ) : discS;
   const double sq = pin(sqrt_ns((double)disc));
   const double nb = (double)(-B);
   const bool qlin = isQ & lin;
-  const double n1q = pin(nb - sq), n1l = pin(-1.0 * (double)cq), n1p = pin((double)(-numP));
+  const double n1q = pin(nb - sq), n1p = pin((double)(-numP));
+  const double n1l = kQuad ? pin(-1.0 * (double)cq) : 0.0;
   const double num1 = isP ? n1p : (qlin ? n1l : n1q);
-  const double den1 = isP ? (double)denP : (qlin ? (double)bq : (isS ? rk.den : 2.0 * (double)aq));
+  const double den1 =
+      isP ? (double)denP : (qlin ? (double)bq : ((isS || !kQuad) ? rk.den : 2.0 * (double)aq));
   const double num2 = nb + sq;
   const float q1 = (float)pin(num1 / den1);
   const float q2 = (float)pin(num2 / den1);
@@ -758,29 +765,34 @@ __device__ __forceinline__ bool test_unified(const rc_shape& s, V3 O, V3 D, RayK
   return ok;
 }
 
-// hit_frame() without type branches; `s` is the winner's record.
+// hit_frame() without type branches; `s` is the winner's record.  kQuad as in test_unified.
+template <bool kQuad>
 __device__ __forceinline__ void hit_frame_sel(const rc_shape& s, V3 O, V3 D, float t, V3& P,
                                               V3& N) {
   P = v3(O.x + D.x * t, O.y + D.y * t, O.z + D.z * t);
   const int type = s.type;
   const float inv = s.inv_r;
   const V3 vs = v3((P.x - s.p[0]) * inv, (P.y - s.p[1]) * inv, (P.z - s.p[2]) * inv);
-  double n0 = 2.0 * s.A * (double)P.x;
-  n0 = n0 + (double)(s.qd * P.y);
-  n0 = n0 + (double)(s.qe * P.z);
-  n0 = n0 + (double)s.qg;
-  double n1 = 2.0 * s.B * (double)P.y;
-  n1 = n1 + (double)(s.qd * P.x);
-  n1 = n1 + (double)(s.qf * P.z);
-  n1 = n1 + (double)s.qh;
-  double n2 = 2.0 * s.C * (double)P.z;
-  n2 = n2 + (double)(s.qe * P.x);
-  n2 = n2 + (double)(s.qf * P.y);
-  n2 = n2 + (double)s.qi;
   const bool isS = type == RC_SHAPE_SPHERE, isP = type == RC_SHAPE_PLANE;
-  const V3 v = sel(isS, vs, v3((float)n0, (float)n1, (float)n2));
+  V3 v = vs;
+  if constexpr (kQuad) {
+    double n0 = 2.0 * s.A * (double)P.x;
+    n0 = n0 + (double)(s.qd * P.y);
+    n0 = n0 + (double)(s.qe * P.z);
+    n0 = n0 + (double)s.qg;
+    double n1 = 2.0 * s.B * (double)P.y;
+    n1 = n1 + (double)(s.qd * P.x);
+    n1 = n1 + (double)(s.qf * P.z);
+    n1 = n1 + (double)s.qh;
+    double n2 = 2.0 * s.C * (double)P.z;
+    n2 = n2 + (double)(s.qe * P.x);
+    n2 = n2 + (double)(s.qf * P.y);
+    n2 = n2 + (double)s.qi;
+    v = sel(isS, vs, v3((float)n0, (float)n1, (float)n2));
+  }
   V3 n = normalize_sel(v);
-  n = sel(!isS && dot(n, D) > 0.0f, v3(n.x * -1.0f, n.y * -1.0f, n.z * -1.0f), n);
+  // quadric normals face the ray (a plane's own normal is taken below, unflipped)
+  if constexpr (kQuad) n = sel(!isS && dot(n, D) > 0.0f, v3(n.x * -1.0f, n.y * -1.0f, n.z * -1.0f), n);
   N = sel(isP, v3(s.n[0], s.n[1], s.n[2]), n);
 }
 
@@ -792,8 +804,9 @@ __device__ __forceinline__ void hit_frame_sel(const rc_shape& s, V3 O, V3 D, flo
 // levels retire in one step.  The carry creep of dense segments alternates hit/miss, so
 // five levels retire in three steps.  Each step is one basic block (selects, no branches)
 // so the scheduler can overlap the independent chains of a lone wave.  GT = the group size
-// as a compile-time constant (4, 8, 16), or 0 for the runtime value Grt.
-template <int GT>
+// as a compile-time constant (4, 8, 16), or 0 for the runtime value Grt; kQuad = the scene has
+// quadrics (test_unified).
+template <int GT, bool kQuad>
 __device__ __forceinline__ V3 carry_path_spec(const Scene& sc, const LaneShape& ls, int kself,
                                               int Grt, int half, const DepRec& r, int maxrec,
                                               V3 c, int& zero_events
@@ -820,7 +833,7 @@ __device__ __forceinline__ V3 carry_path_spec(const Scene& sc, const LaneShape& 
     const int myS = half ? -1 : S;
     const RayK rk = ray_consts(myD);
     float tt = 0.0f;
-    const bool ok = test_unified(ls.s, C, myD, rk, myS, tt) && ls.has && kself != myS &&
+    const bool ok = test_unified<kQuad>(ls.s, C, myD, rk, myS, tt) && ls.has && kself != myS &&
                     __builtin_inff() > tt && tt > 0.0f;
     float t = ok ? tt : __builtin_inff();
     int k = ok ? kself : kNone;
@@ -849,7 +862,7 @@ __device__ __forceinline__ V3 carry_path_spec(const Scene& sc, const LaneShape& 
     const V3 Dw = sel(two, D2, D1);
     const bool hit = w != kNone;
     V3 P, Nw;
-    hit_frame_sel(sc.shapes[hit ? w : 0], C, Dw, tw, P, Nw);
+    hit_frame_sel<kQuad>(sc.shapes[hit ? w : 0], C, Dw, tw, P, Nw);
     C = sel(hit, P, C);
     N = sel(hit, Nw, N);
     obj = hit ? w : obj;

@@ -17,6 +17,7 @@ struct LaunchScene {
   int n, m;
   float cam_w, cam_h;
   unsigned long long refl_mask;   // bit k: shape k reflective (n <= 64)
+  int has_quadric;                // the scene has a quadric
 };
 
 // Parity-mode workspace (device pointers), sized for W*H pixels.

@@ -429,10 +429,11 @@ __device__ __forceinline__ int wave_window(const Scene& sc, int maxrec,
     const DepRec ri = shfl_rec(r, i < 64 ? i : 63);
     V3 oc = c;
 #if RC_STAMPS
-#define RC_SPEC(GT) carry_path_spec<GT>(sc, ls, kself, G, half, ri, maxrec, c, zero, st_)
+#define RC_SPEC1(GT, Q) carry_path_spec<GT, Q>(sc, ls, kself, G, half, ri, maxrec, c, zero, st_)
 #else
-#define RC_SPEC(GT) carry_path_spec<GT>(sc, ls, kself, G, half, ri, maxrec, c, zero)
+#define RC_SPEC1(GT, Q) carry_path_spec<GT, Q>(sc, ls, kself, G, half, ri, maxrec, c, zero)
 #endif
+#define RC_SPEC(GT) (sc.has_quadric ? RC_SPEC1(GT, true) : RC_SPEC1(GT, false))
     if (act) {
       if (G == 8) oc = RC_SPEC(8);
       else if (G == 4) oc = RC_SPEC(4);
@@ -441,6 +442,7 @@ __device__ __forceinline__ int wave_window(const Scene& sc, int maxrec,
       else oc = carry_path_coop(sc, ls, kself, G, ri, maxrec, c, zero);
     }
 #undef RC_SPEC
+#undef RC_SPEC1
     const unsigned long long mc = __ballot(act && (lane % GE) == 0 && !same_bits(oc, c));
     if (mc == 0) {
       const int lim = pos + E < nvalid ? pos + E : nvalid;
@@ -592,10 +594,11 @@ __device__ __forceinline__ void block_window(const Scene& sc, int maxrec, BlockW
       V3 oc = c;
 #if RC_STAMPS
       Stamps stq = {{0, 0, 0, 0}, 0};
-#define RC_SPEC(GT) carry_path_spec<GT>(sc, ls, kself, G, half, ri, maxrec, c, zero, &stq)
+#define RC_SPEC1(GT, Q) carry_path_spec<GT, Q>(sc, ls, kself, G, half, ri, maxrec, c, zero, &stq)
 #else
-#define RC_SPEC(GT) carry_path_spec<GT>(sc, ls, kself, G, half, ri, maxrec, c, zero)
+#define RC_SPEC1(GT, Q) carry_path_spec<GT, Q>(sc, ls, kself, G, half, ri, maxrec, c, zero)
 #endif
+#define RC_SPEC(GT) (sc.has_quadric ? RC_SPEC1(GT, true) : RC_SPEC1(GT, false))
       if (act) {
         if (G == 8) oc = RC_SPEC(8);
         else if (G == 4) oc = RC_SPEC(4);
@@ -604,6 +607,7 @@ __device__ __forceinline__ void block_window(const Scene& sc, int maxrec, BlockW
         else oc = carry_path_coop(sc, ls, kself, G, ri, maxrec, c, zero);
       }
 #undef RC_SPEC
+#undef RC_SPEC1
       const unsigned long long mc = __ballot(act && (lane % GE) == 0 && !same_bits(oc, c));
       const int g = mc ? (__ffsll((long long)mc) - 1) / GE : -1;
       if (lane == 0) bw.wpos[par][wave] = g >= 0 ? pos + wave * E + g : kNo;
@@ -893,7 +897,8 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
         trace[3 * s + 2] = (unsigned)(__builtin_amdgcn_s_memtime() - c_seg);
       }
     }
-    return;
+    // the team's segments are done: its waves join the regular queue (every wave from here
+    // on is independent; a frame without long segments gets the whole grid)
   }
 
   // ------------------------------------------------------------- regular waves --
@@ -1116,6 +1121,7 @@ static Scene make_scene(const LaunchScene& s) {
   sc.n = s.n;
   sc.m = s.m;
   sc.refl_mask = s.refl_mask;
+  sc.has_quadric = s.has_quadric;
   return sc;
 }
 static Cam make_cam(const LaunchScene& s, int W, int H) {

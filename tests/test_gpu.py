@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 
 from helpers import (GOLDEN, ROOT, file_md5, golden_key, golden_table, oracle_render, p3_md5,
-                     rc, scene_path)
+                     random_scene, rc, scene_path)
 
 pytestmark = pytest.mark.gpu
 
@@ -70,6 +70,24 @@ def test_parity_schedules(knob, scenes, table, monkeypatch):
         w, h = map(int, size.split("x"))
         img = rc.render(scenes[scene], w, h, depth=int(d[1:]), mode=mode)
         assert p3_md5(img) == table[key]["md5"], (knob, key)
+
+
+@pytest.mark.parametrize("n_shapes", [20, 33, 64, 65, 90])
+def test_many_shapes_vs_oracle(n_shapes, tmp_path):
+    """Scenes beyond the examples' sizes: 32-lane groups, the non-speculative cooperative
+    evaluator (64 lanes per entry), the resolver without LDS-staged shapes (> 64) and the
+    reflectivity test without the bitmask — against the CPU oracle, every depth class."""
+    rng = np.random.default_rng(1000 + n_shapes)
+    path = str(tmp_path / f"m{n_shapes}.scene")
+    random_scene(rng, path, n_shapes, 2)
+    s = rc.Scene.from_file(path)
+    for mode in ("parity", "fast"):
+        for d in (1, 4, 6):
+            want, st = oracle_render(s, 96, 72, d, mode)
+            if not st["parity_defined"]:
+                continue
+            np.testing.assert_array_equal(rc.render(s, 96, 72, depth=d, mode=mode), want,
+                                          err_msg=f"{n_shapes} shapes {mode} d{d}")
 
 
 def test_c5_8192(scenes, table):

@@ -11,7 +11,7 @@ import numpy as np
 import pytest
 
 from helpers import (GOLDEN, SCENES, golden_key, golden_table, have_ref, oracle_render, p3_md5,
-                     rc, run_ref, scene_path)
+                     rc, run_ref, scene_path, random_scene)
 
 SMALL = ["simple", "reflection", "quadric", "example2", "example3", "quadric2"]
 
@@ -68,52 +68,12 @@ def test_oracle_stats_match_survey():
     assert st["parity_defined"] == 1
 
 
-def _random_scene(rng, path, n_shapes, n_lights):
-    """A phantom-safe random scene in the reference grammar (lights keep the phantom black:
-    1 light with color[0]+color[1] >= 1; 2 lights with L1.pos.y + L1.pos.z >= 1)."""
-    lines = ["camera, width: 2.0, height: 2.0"]
-    for _ in range(n_shapes):
-        kind = rng.choice(["sphere", "sphere", "plane", "quadric"])
-        dif = ", ".join(f"{v:.3f}" for v in rng.uniform(0, 1, 3))
-        spe = ", ".join(f"{v:.3f}" for v in rng.uniform(0, 1, 3))
-        refl = rng.uniform(0, 0.8)
-        if kind == "sphere":
-            pos = [rng.uniform(-4, 4), rng.uniform(-3, 3), rng.uniform(-15, -4)]
-            lines.append(f"sphere, radius: {rng.uniform(0.3, 2.0):.3f}, diffuse_color: [{dif}], "
-                         f"specular_color: [{spe}], position: [{pos[0]:.3f}, {pos[1]:.3f}, "
-                         f"{pos[2]:.3f}], reflectivity: {refl:.3f}, refractivity: "
-                         f"{rng.uniform(0, 0.2):.3f}, ior: 1.33")
-        elif kind == "plane":
-            nrm = rng.normal(size=3)
-            nrm[1] = abs(nrm[1]) + 1
-            lines.append(f"plane, normal: [{nrm[0]:.3f}, {nrm[1]:.3f}, {nrm[2]:.3f}], "
-                         f"diffuse_color: [{dif}], position: [0, {rng.uniform(-5, -1):.3f}, 0], "
-                         f"reflectivity: {refl:.3f}")
-        else:
-            a, b, c = rng.uniform(-1, 4, 3)
-            g, h, i = rng.uniform(-20, 20, 3)
-            lines.append(f"quadric, diffuse_color: [{dif}], specular_color: [{spe}], a: {a:.2f}, "
-                         f"b: {b:.2f}, c: {c:.2f}, d: 0, e: 0, f: 0, g: {g:.2f}, h: {h:.2f}, "
-                         f"i: {i:.2f}, j: {rng.uniform(50, 300):.2f}, reflectivity: {refl:.3f}")
-    for k in range(n_lights):
-        col = rng.uniform(0.6, 4, 3)
-        pos = [rng.uniform(-10, 10), rng.uniform(1, 10), rng.uniform(-10, 2)]
-        spot = n_lights == 2 and k == 0 and rng.uniform() < 0.5
-        extra = (f", theta: {rng.uniform(1, 20):.2f}, angular-a0: {int(rng.integers(0, 4))}, "
-                 f"direction: [0, 0, -1]") if spot else ""
-        lines.append(f"light, color: [{col[0]:.2f}, {col[1]:.2f}, {col[2]:.2f}], radial-a2: 0.01, "
-                     f"radial-a1: 0.0125, radial-a0: 0.0125, position: [{pos[0]:.2f}, "
-                     f"{pos[1]:.2f}, {pos[2]:.2f}]{extra}")
-    with open(path, "w") as f:
-        f.write("\n".join(lines) + "\n")
-
-
 @pytest.mark.skipif(not have_ref(), reason="oracle/_ref not built (make ref)")
 @pytest.mark.parametrize("seed", range(8))
 def test_oracle_vs_reference_random_scenes(seed, tmp_path):
     rng = np.random.default_rng(seed)
     path = str(tmp_path / f"r{seed}.scene")
-    _random_scene(rng, path, int(rng.integers(2, 9)), int(rng.integers(1, 3)))
+    random_scene(rng, path, int(rng.integers(2, 9)), int(rng.integers(1, 3)))
     s = rc.Scene.from_file(path)
     for mode in ("parity", "fast"):
         for d in (1, 6):
@@ -121,6 +81,21 @@ def test_oracle_vs_reference_random_scenes(seed, tmp_path):
             if not st["parity_defined"]:
                 continue
             np.testing.assert_array_equal(img, run_ref(path, 48, 40, d, mode))
+
+
+@pytest.mark.skipif(not have_ref(), reason="oracle/_ref not built (make ref)")
+@pytest.mark.parametrize("n_shapes", [20, 33, 64, 65, 90])
+def test_oracle_vs_reference_many_shapes(n_shapes, tmp_path):
+    """Scenes larger than the examples (the GPU evaluator groups 32 / 64 lanes per entry
+    and stops staging shapes in LDS above 64): the oracle still equals the reference."""
+    rng = np.random.default_rng(1000 + n_shapes)
+    path = str(tmp_path / f"m{n_shapes}.scene")
+    random_scene(rng, path, n_shapes, 2)
+    s = rc.Scene.from_file(path)
+    for mode in ("parity", "fast"):
+        img, st = oracle_render(s, 40, 32, 6, mode)
+        if st["parity_defined"]:
+            np.testing.assert_array_equal(img, run_ref(path, 40, 32, 6, mode))
 
 
 @pytest.mark.skipif(not have_ref(), reason="oracle/_ref not built (make ref)")
