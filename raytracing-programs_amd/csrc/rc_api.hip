@@ -183,20 +183,11 @@ int upload_scene(DevCtx& c, const rc_scene* s, rc::LaunchScene& ls) {
   ls.cam_h = h->cam_h;
   ls.refl_mask = 0;
   ls.has_quadric = 0;
-  ls.no_cross = 0;
   const rc_shape* hs = (const rc_shape*)((const char*)h + h->off_shapes);
   for (int k = 0; k < h->n && k < 64; ++k)
     if (hs[k].refl > 0.0f) ls.refl_mask |= 1ull << k;
-  ls.no_cross = 1;
-  for (int k = 0; k < h->n; ++k) {
-    if (hs[k].type != RC_SHAPE_QUADRIC) continue;
-    ls.has_quadric = 1;
-    unsigned bits[3];
-    std::memcpy(&bits[0], &hs[k].qd, 4);
-    std::memcpy(&bits[1], &hs[k].qe, 4);
-    std::memcpy(&bits[2], &hs[k].qf, 4);
-    if (bits[0] | bits[1] | bits[2]) ls.no_cross = 0;   // +0.0 only: -0.0 keeps the terms
-  }
+  for (int k = 0; k < h->n; ++k)
+    if (hs[k].type == RC_SHAPE_QUADRIC) ls.has_quadric = 1;
   return 0;
 }
 

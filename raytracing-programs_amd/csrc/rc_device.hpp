@@ -39,7 +39,6 @@ struct Scene {
   int n, m;
   unsigned long long refl_mask;          // bit k: shape k has reflectivity > 0 (k < 64)
   int has_quadric;                       // any quadric: picks the evaluator specialisation
-  int no_cross;                          // every quadric has d = e = f = +0.0 (bitwise)
 };
 
 // refl[obj] > 0 (C/raycast.c:352) from a register bitmask when n <= 64
@@ -687,18 +686,9 @@ __device__ __forceinline__ unsigned long long stamp_now() {
 // The plane's f32 quotient (-num)/den is taken as (float)((double)(-num) / (double)den):
 // double rounding is innocuous for division when 53 >= 2*24 + 2.
 
-__device__ __forceinline__ bool finite3(float a, float b, float c) {
-  return __builtin_isfinite(a) & __builtin_isfinite(b) & __builtin_isfinite(c);
-}
-
 // test_shape() for any type, branch-free.  kQuad = false: the scene has no quadric, so the
-// quadric part is compiled out (every quadric term below is dead).  kNoCross: every quadric
-// has d = e = f = +0.0, so each d/e/f term is +-0 — or NaN, exactly when one of its float
-// factors is not finite (0 * inf): (d*x)*y is NaN iff x or y is; d*(x*y' + y*x') iff the
-// inner sum is.  The terms are left out and the NaN cases restored by selects; what remains
-// different is only the sign of a zero accumulator, which no consumer of aq, bq, cq
-// distinguishes (the roots, the linear case and every comparison treat +0 and -0 alike).
-template <bool kQuad, bool kNoCross = false>
+// quadric part is compiled out (every quadric term below is dead).
+template <bool kQuad>
 __device__ __forceinline__ bool test_unified(const rc_shape& s, V3 O, V3 D, RayK rk, int skip,
                                              float& t) {
   const int type = s.type;
@@ -720,11 +710,9 @@ __device__ __forceinline__ bool test_unified(const rc_shape& s, V3 O, V3 D, RayK
     acc = s.A * ((double)O.x * (double)O.x);
     acc = acc + s.B * ((double)O.y * (double)O.y);
     acc = acc + s.C * ((double)O.z * (double)O.z);
-    if (!kNoCross) {
-      acc = acc + (double)(s.qd * O.x * O.y);
-      acc = acc + (double)(s.qe * O.x * O.z);
-      acc = acc + (double)(s.qf * O.y * O.z);
-    }
+    acc = acc + (double)(s.qd * O.x * O.y);
+    acc = acc + (double)(s.qe * O.x * O.z);
+    acc = acc + (double)(s.qf * O.y * O.z);
     acc = acc + (double)(s.qg * O.x);
     acc = acc + (double)(s.qh * O.y);
     acc = acc + (double)(s.qi * O.z);
@@ -733,32 +721,20 @@ __device__ __forceinline__ bool test_unified(const rc_shape& s, V3 O, V3 D, RayK
     acc = s.A * ((double)D.x * (double)D.x);
     acc = acc + s.B * ((double)D.y * (double)D.y);
     acc = acc + s.C * ((double)D.z * (double)D.z);
-    if (!kNoCross) {
-      acc = acc + (double)(s.qd * D.x * D.y);
-      acc = acc + (double)(s.qe * D.x * D.z);
-      acc = acc + (double)(s.qf * D.y * D.z);
-    }
+    acc = acc + (double)(s.qd * D.x * D.y);
+    acc = acc + (double)(s.qe * D.x * D.z);
+    acc = acc + (double)(s.qf * D.y * D.z);
     aq = (float)acc;
     acc = 2.0 * s.A * (double)O.x * (double)D.x;
     acc = acc + 2.0 * s.B * (double)O.y * (double)D.y;
     acc = acc + 2.0 * s.C * (double)O.z * (double)D.z;
-    if (!kNoCross) {
-      acc = acc + (double)(s.qd * (O.x * D.y + O.y * D.x));
-      acc = acc + (double)(s.qe * (O.x * D.z + O.z * D.x));
-      acc = acc + (double)(s.qf * (O.y * D.z + O.z * D.y));
-    }
+    acc = acc + (double)(s.qd * (O.x * D.y + O.y * D.x));
+    acc = acc + (double)(s.qe * (O.x * D.z + O.z * D.x));
+    acc = acc + (double)(s.qf * (O.y * D.z + O.z * D.y));
     acc = acc + (double)(s.qg * D.x);
     acc = acc + (double)(s.qh * D.y);
     acc = acc + (double)(s.qi * D.z);
     bq = (float)acc;
-    if (kNoCross) {   // the left-out d/e/f terms' NaN cases (see above)
-      const float nan = __builtin_nanf("");
-      const float sxy = O.x * D.y + O.y * D.x, sxz = O.x * D.z + O.z * D.x,
-                  syz = O.y * D.z + O.z * D.y;
-      cq = finite3(O.x, O.y, O.z) ? cq : nan;
-      aq = finite3(D.x, D.y, D.z) ? aq : nan;
-      bq = finite3(sxy, sxz, syz) ? bq : nan;
-    }
     discQ = (float)((double)bq * (double)bq - 4.0 * (double)aq * (double)cq);
     lin = (double)aq == 0.0;
   }
@@ -789,10 +765,8 @@ __device__ __forceinline__ bool test_unified(const rc_shape& s, V3 O, V3 D, RayK
   return ok;
 }
 
-// hit_frame() without type branches; `s` is the winner's record.  kQuad, kNoCross as in
-// test_unified (a gradient component's d/e/f terms are NaN iff one of the other two P
-// components is not finite).
-template <bool kQuad, bool kNoCross = false>
+// hit_frame() without type branches; `s` is the winner's record.  kQuad as in test_unified.
+template <bool kQuad>
 __device__ __forceinline__ void hit_frame_sel(const rc_shape& s, V3 O, V3 D, float t, V3& P,
                                               V3& N) {
   P = v3(O.x + D.x * t, O.y + D.y * t, O.z + D.z * t);
@@ -803,29 +777,18 @@ __device__ __forceinline__ void hit_frame_sel(const rc_shape& s, V3 O, V3 D, flo
   V3 v = vs;
   if constexpr (kQuad) {
     double n0 = 2.0 * s.A * (double)P.x;
-    double n1 = 2.0 * s.B * (double)P.y;
-    double n2 = 2.0 * s.C * (double)P.z;
-    if (!kNoCross) {
-      n0 = n0 + (double)(s.qd * P.y);
-      n0 = n0 + (double)(s.qe * P.z);
-      n1 = n1 + (double)(s.qd * P.x);
-      n1 = n1 + (double)(s.qf * P.z);
-      n2 = n2 + (double)(s.qe * P.x);
-      n2 = n2 + (double)(s.qf * P.y);
-    }
+    n0 = n0 + (double)(s.qd * P.y);
+    n0 = n0 + (double)(s.qe * P.z);
     n0 = n0 + (double)s.qg;
+    double n1 = 2.0 * s.B * (double)P.y;
+    n1 = n1 + (double)(s.qd * P.x);
+    n1 = n1 + (double)(s.qf * P.z);
     n1 = n1 + (double)s.qh;
+    double n2 = 2.0 * s.C * (double)P.z;
+    n2 = n2 + (double)(s.qe * P.x);
+    n2 = n2 + (double)(s.qf * P.y);
     n2 = n2 + (double)s.qi;
-    float f0 = (float)n0, f1 = (float)n1, f2 = (float)n2;
-    if (kNoCross) {
-      const float nan = __builtin_nanf("");
-      const bool fx = __builtin_isfinite(P.x), fy = __builtin_isfinite(P.y),
-                 fz = __builtin_isfinite(P.z);
-      f0 = (fy & fz) ? f0 : nan;
-      f1 = (fx & fz) ? f1 : nan;
-      f2 = (fx & fy) ? f2 : nan;
-    }
-    v = sel(isS, vs, v3(f0, f1, f2));
+    v = sel(isS, vs, v3((float)n0, (float)n1, (float)n2));
   }
   V3 n = normalize_sel(v);
   // quadric normals face the ray (a plane's own normal is taken below, unflipped)
@@ -842,9 +805,8 @@ __device__ __forceinline__ void hit_frame_sel(const rc_shape& s, V3 O, V3 D, flo
 // five levels retire in three steps.  Each step is one basic block (selects, no branches)
 // so the scheduler can overlap the independent chains of a lone wave.  GT = the group size
 // as a compile-time constant (4, 8, 16), or 0 for the runtime value Grt; kQuad = the scene has
-// quadrics, kNoCross = they have no d/e/f terms (test_unified: used while the operands are
-// bounded on every lane, otherwise the step takes the full form).
-template <int GT, bool kQuad, bool kNoCross = false>
+// quadrics (test_unified).
+template <int GT, bool kQuad>
 __device__ __forceinline__ V3 carry_path_spec(const Scene& sc, const LaneShape& ls, int kself,
                                               int Grt, int half, const DepRec& r, int maxrec,
                                               V3 c, int& zero_events
@@ -871,8 +833,8 @@ __device__ __forceinline__ V3 carry_path_spec(const Scene& sc, const LaneShape& 
     const int myS = half ? -1 : S;
     const RayK rk = ray_consts(myD);
     float tt = 0.0f;
-    const bool hitk = test_unified<kQuad, kNoCross>(ls.s, C, myD, rk, myS, tt);
-    const bool ok = hitk && ls.has && kself != myS && __builtin_inff() > tt && tt > 0.0f;
+    const bool ok = test_unified<kQuad>(ls.s, C, myD, rk, myS, tt) && ls.has && kself != myS &&
+                    __builtin_inff() > tt && tt > 0.0f;
     float t = ok ? tt : __builtin_inff();
     int k = ok ? kself : kNone;
     RC_STAMP(1);
@@ -900,7 +862,7 @@ __device__ __forceinline__ V3 carry_path_spec(const Scene& sc, const LaneShape& 
     const V3 Dw = sel(two, D2, D1);
     const bool hit = w != kNone;
     V3 P, Nw;
-    hit_frame_sel<kQuad, kNoCross>(sc.shapes[hit ? w : 0], C, Dw, tw, P, Nw);
+    hit_frame_sel<kQuad>(sc.shapes[hit ? w : 0], C, Dw, tw, P, Nw);
     C = sel(hit, P, C);
     N = sel(hit, Nw, N);
     obj = hit ? w : obj;

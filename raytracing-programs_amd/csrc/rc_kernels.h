@@ -18,7 +18,6 @@ struct LaunchScene {
   float cam_w, cam_h;
   unsigned long long refl_mask;   // bit k: shape k reflective (n <= 64)
   int has_quadric;                // the scene has a quadric
-  int no_cross;                   // every quadric has d = e = f = +0.0 (bitwise)
 };
 
 // Parity-mode workspace (device pointers), sized for W*H pixels.

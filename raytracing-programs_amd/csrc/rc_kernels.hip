@@ -429,11 +429,11 @@ __device__ __forceinline__ int wave_window(const Scene& sc, int maxrec,
     const DepRec ri = shfl_rec(r, i < 64 ? i : 63);
     V3 oc = c;
 #if RC_STAMPS
-#define RC_SPEC1(GT, Q, X) carry_path_spec<GT, Q, X>(sc, ls, kself, G, half, ri, maxrec, c, zero, st_)
+#define RC_SPEC1(GT, Q) carry_path_spec<GT, Q>(sc, ls, kself, G, half, ri, maxrec, c, zero, st_)
 #else
-#define RC_SPEC1(GT, Q, X) carry_path_spec<GT, Q, X>(sc, ls, kself, G, half, ri, maxrec, c, zero)
+#define RC_SPEC1(GT, Q) carry_path_spec<GT, Q>(sc, ls, kself, G, half, ri, maxrec, c, zero)
 #endif
-#define RC_SPEC(GT) (sc.has_quadric ? (sc.no_cross ? RC_SPEC1(GT, true, true) : RC_SPEC1(GT, true, false)) : RC_SPEC1(GT, false, false))
+#define RC_SPEC(GT) (sc.has_quadric ? RC_SPEC1(GT, true) : RC_SPEC1(GT, false))
     if (act) {
       if (G == 8) oc = RC_SPEC(8);
       else if (G == 4) oc = RC_SPEC(4);
@@ -594,11 +594,11 @@ __device__ __forceinline__ void block_window(const Scene& sc, int maxrec, BlockW
       V3 oc = c;
 #if RC_STAMPS
       Stamps stq = {{0, 0, 0, 0}, 0};
-#define RC_SPEC1(GT, Q, X) carry_path_spec<GT, Q, X>(sc, ls, kself, G, half, ri, maxrec, c, zero, &stq)
+#define RC_SPEC1(GT, Q) carry_path_spec<GT, Q>(sc, ls, kself, G, half, ri, maxrec, c, zero, &stq)
 #else
-#define RC_SPEC1(GT, Q, X) carry_path_spec<GT, Q, X>(sc, ls, kself, G, half, ri, maxrec, c, zero)
+#define RC_SPEC1(GT, Q) carry_path_spec<GT, Q>(sc, ls, kself, G, half, ri, maxrec, c, zero)
 #endif
-#define RC_SPEC(GT) (sc.has_quadric ? (sc.no_cross ? RC_SPEC1(GT, true, true) : RC_SPEC1(GT, true, false)) : RC_SPEC1(GT, false, false))
+#define RC_SPEC(GT) (sc.has_quadric ? RC_SPEC1(GT, true) : RC_SPEC1(GT, false))
       if (act) {
         if (G == 8) oc = RC_SPEC(8);
         else if (G == 4) oc = RC_SPEC(4);
@@ -1122,7 +1122,6 @@ static Scene make_scene(const LaunchScene& s) {
   sc.m = s.m;
   sc.refl_mask = s.refl_mask;
   sc.has_quadric = s.has_quadric;
-  sc.no_cross = s.no_cross;
   return sc;
 }
 static Cam make_cam(const LaunchScene& s, int W, int H) {
