@@ -124,6 +124,9 @@ def main():
     ap.add_argument("--depth", type=int, default=6)
     ap.add_argument("--scene", default="quadric")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--inflight", type=int, default=2, choices=[1, 2],
+                    help="parity frames in flight: 2 = rc_frame_submit (the next frame's pixel "
+                         "phases beside this frame's resolver), 1 = one rc_render_device per step")
     args = ap.parse_args()
 
     import torch
@@ -153,7 +156,19 @@ def main():
         send = torch.zeros((rows_max, W, 3), dtype=torch.uint8, device="cuda")
         full = torch.empty((rows_max * world, W, 3), dtype=torch.uint8, device="cuda")
 
+    piped = mode == "parity" and args.depth > 0 and args.inflight == 2 and not sharded
+    if piped:   # every frame of the timed region gets its own output image
+        outs = [torch.empty((H, W, 3), dtype=torch.uint8, device="cuda")
+                for _ in range(max(args.steps, 1))]
+        torch.cuda.synchronize()
+    frame_no = [0]
+
     def step():
+        if piped:
+            buf = outs[frame_no[0] % len(outs)]
+            frame_no[0] += 1
+            pkg.frame_submit(scene, W, H, buf.data_ptr(), depth=args.depth, mode=mode)
+            return
         if sharded:
             pkg.render_device(scene, W, H, send.data_ptr(), stream.cuda_stream, depth=args.depth,
                               mode=mode, row0=row0, row_step=step_rows, nrows=nrows)
@@ -164,22 +179,47 @@ def main():
             pkg.render_device(scene, W, H, out.data_ptr(), stream.cuda_stream, depth=args.depth,
                               mode=mode)
 
+    def drain():
+        if piped:
+            pkg.frames_wait(pipe_tim)
+        torch.cuda.synchronize()
+
+    pipe_tim = {}
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize()
+    drain()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     pkg.profile_begin()
+    frame_no[0] = 0
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-    torch.cuda.synchronize()
+    drain()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     phases = pkg.profile_end()
+    single = None
+    if piped:
+        # per-phase times and latency of a lone frame (rc_render_device), for the record
+        for _ in range(2):
+            pkg.render_device(scene, W, H, out.data_ptr(), stream.cuda_stream,
+                              depth=args.depth, mode=mode)
+        torch.cuda.synchronize()
+        pkg.profile_begin()
+        ts = time.perf_counter()
+        for _ in range(5):
+            pkg.render_device(scene, W, H, out.data_ptr(), stream.cuda_stream,
+                              depth=args.depth, mode=mode)
+        torch.cuda.synchronize()
+        single_ms = (time.perf_counter() - ts) * 1e3 / 5
+        phases = pkg.profile_end()
+        single = {"ms": round(single_ms, 4), "value": round(W * H / (single_ms * 1e-3), 1),
+                  "resolve_ms_in_flight": round(pipe_tim.get("resolve_ms", 0.0), 4),
+                  "note": "one frame at a time (rc_render_device), phases_ms are its phases"}
     tmax = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
     if world > 1:
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
@@ -197,6 +237,8 @@ def main():
         parity = mode == "parity" and args.depth > 0
         if parity:
             dom_name, dom_ms = "k_resolve", phases["resolve_ms"]
+            if piped and pipe_tim.get("resolve_ms"):   # the launches of the timed region
+                dom_ms = pipe_tim["resolve_ms"]
             dom_flop = work["dep_flop_per_entry"] * tim["dep_pixels"] if work else None
             render_ms = phases["phase_a_ms"] + phases["phase_c_ms"]
         else:
@@ -225,7 +267,8 @@ def main():
                                    + (", byte-identical to C/raycast.c" if mode == "parity" else ""),
                        "mode": mode, "width": W, "height": H, "depth": args.depth,
                        "parallelism": (f"rows-cyclic x{world} + RCCL all_gather" if sharded else
-                                       (f"replicas x{world}" if world > 1 else "single GPU"))},
+                                       (f"replicas x{world}" if world > 1 else "single GPU")),
+                       "frames_in_flight": 2 if piped else 1},
             "phases_ms": {k: round(v, 4) for k, v in phases.items() if k.endswith("_ms")},
             "dep_pixels": tim.get("dep_pixels"),
             "roofline": {"bound": "valu", "kernel": dom_name,
@@ -249,6 +292,8 @@ def main():
                              if phases["total_ms"] else None,
                              "peak": PEAK_HBM_GBS, "unit": "GB/s"},
         }
+        if single:
+            line["single_frame"] = single
         if world == 1 and not sharded:
             line["end_to_end"] = end_to_end(pkg, scene, W, H, args.depth, mode)
         if world == 1 and not args.no_cpu_baseline:

@@ -166,10 +166,27 @@ int rc_render(const rc_scene *scene, int width, int height, const rc_options *op
 /* Device-resident render on the current device: rows row0, row0+row_step, ... (nrows rows)
  * of a W x H image into d_out (nrows*W*3 bytes, device memory, compact row order) on the
  * given HIP stream (NULL = default stream).  Parity mode requires row0=0,row_step=1,nrows=H.
- * Asynchronous except for the parity resolver's host handshake.  Returns 0 on success. */
+ * Asynchronous unless timing is requested.  Returns 0 on success. */
 int rc_render_device(const rc_scene *scene, int width, int height, int row0, int row_step,
                      int nrows, const rc_options *opt, uint8_t *d_out, void *stream,
                      rc_timing *timing);
+
+/* Frames in flight (an extension for rendering frame sequences; no reference
+ * counterpart).  rc_frame_submit enqueues one whole W x H image of `scene` into d_out
+ * (W*H*3 bytes, device memory, ready for use: synchronise the stream that produced it
+ * first) and returns.  It is byte-identical to rc_render_device's.  In parity mode up to
+ * two frames are in flight on the current device.  The device's CUs are split in two
+ * partitions (hipExtStreamCreateWithCUMask; RC_PIPE_RES_CUS sets the resolver's share).
+ * One runs the frames' carry resolvers in submission order.  The other runs the next frame's
+ * phase A and compaction and the previous frame's phase C beside it.  A frame then costs
+ * about its resolver's time instead of the sum of its phases.  Fast mode (no serial stage)
+ * renders the frames back to back on the whole device.  rc_frames_wait blocks until every
+ * submitted frame is complete.  It reports a failed resolver hand-off (returns -1) and fills
+ * *timing (may be NULL): resolve_ms = mean resolver span; dep_pixels and zero_normalize of
+ * the last frame. */
+int rc_frame_submit(const rc_scene *scene, int width, int height, const rc_options *opt,
+                    uint8_t *d_out);
+int rc_frames_wait(rc_timing *timing);
 
 /* Duration (ms) of the last call's dominant kernel on the current device (the carry
  * resolver in parity mode, the render kernel otherwise), from HIP events on its stream. */

@@ -116,6 +116,9 @@ def hip_lib():
     lib.rc_render_device.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                      ctypes.c_int, ctypes.c_int, ctypes.POINTER(RcOptions),
                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(RcTiming)]
+    lib.rc_frame_submit.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                    ctypes.POINTER(RcOptions), ctypes.c_void_p]
+    lib.rc_frames_wait.argtypes = [ctypes.POINTER(RcTiming)]
     lib.rc_last_kernel_ms.restype = ctypes.c_double
     lib.rc_version.restype = ctypes.c_char_p
     lib.rc_default_options.argtypes = [ctypes.POINTER(RcOptions), ctypes.c_int]
@@ -241,6 +244,24 @@ def render_device(scene, width, height, d_out_ptr, stream_ptr=None, depth=6, mod
                               ctypes.byref(t) if timing is not None else None)
     if rc != 0:
         raise RuntimeError("rc_render_device failed (see stderr)")
+    if timing is not None:
+        timing.update({k: getattr(t, k) for k, _ in RcTiming._fields_})
+
+
+def frame_submit(scene, width, height, d_out_ptr, depth=6, mode="parity"):
+    """Enqueue one whole image into device memory at d_out_ptr (W*H*3 B) with frames in
+    flight (rc_frame_submit); returns at once.  Pair with frames_wait()."""
+    opt = options(depth, mode)
+    if hip_lib().rc_frame_submit(scene.packed(), width, height, ctypes.byref(opt),
+                                 ctypes.c_void_p(d_out_ptr)) != 0:
+        raise RuntimeError("rc_frame_submit failed (see stderr)")
+
+
+def frames_wait(timing=None):
+    """Block until every submitted frame is complete (rc_frames_wait)."""
+    t = RcTiming()
+    if hip_lib().rc_frames_wait(ctypes.byref(t)) != 0:
+        raise RuntimeError("rc_frames_wait failed: a resolver hand-off timed out (see stderr)")
     if timing is not None:
         timing.update({k: getattr(t, k) for k, _ in RcTiming._fields_})
 

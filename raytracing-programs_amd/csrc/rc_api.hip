@@ -10,6 +10,7 @@
 // SURVEY.md §5), each device renders its rows into a compact buffer and a strided 2-D copy
 // drops them straight into their interleaved place in the host pixmap.  The multi-process
 // (one rank per GPU, RCCL gather) path is driven from Python: see bench.py.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <chrono>
@@ -55,10 +56,46 @@ struct DevBuf {
   }
 };
 
+// One frame's device state: the uploaded scene, the zero-normalize counter and the parity
+// workspace.  The plain path has one (DevCtx::fb); pipelined frames alternate two (Pipe).
+struct FrameBufs {
+  unsigned epoch = 0;   // carry-in tag of the last parity frame in this workspace
+  DevBuf zcount;        // zero-normalize counter
+  DevBuf scene;         // uploaded packed scene
+  const void* scene_src = nullptr;   // host image last uploaded
+  DevBuf cls, wcarry, deprec, rows, dep_pix, seg_key, seg_start, seg_order, batch_state, cin,
+      counters, team, trace;
+};
+
+// Pipelined parity frames (rc_frame_submit).  The device's CUs are split in two partitions
+// (hipExtStreamCreateWithCUMask).  Partition A runs the carry resolvers: kLanes resolver
+// streams, each resolver grid sized to A/kLanes CUs (one workgroup per CU), so the resolvers in
+// flight are always wholly resident side by side (a team spins on co-resident workgroups;
+// at most kLanes resolvers are in flight since each stream runs its resolvers in order).
+// Partition B runs every frame's phase A, compaction and phase C on per-slot streams.  A
+// resolver is latency-bound (its carry chains), so overlapping kLanes of them multiplies the
+// frame rate until partition B's pixel work becomes the bound.
+struct Pipe {
+  static constexpr int kSlots = 4;   // frame workspaces (a frame re-uses slot k after k's end)
+  static constexpr int kLanes = 2;   // resolvers in flight
+  bool init = false;
+  int res_cus = 0;                   // CUs in partition A
+  int lanes = kLanes;                // resolver streams in use (RC_PIPE_RESOLVERS)
+  hipStream_t pix[kSlots] = {}, res[kLanes] = {};
+  hipEvent_t ready[kSlots] = {}, done[kSlots] = {};
+  static constexpr int kEv = 64;     // resolver timing events of the last kEv frames
+  hipEvent_t rt[kEv][2] = {};
+  FrameBufs fb[kSlots];
+  long long submitted = 0;           // parity frames since the last rc_frames_wait
+  long long frames = 0;              // frames of any mode since the last rc_frames_wait
+  long long total = 0;               // parity frames ever (slot / stream rotation)
+  long long last = -1;               // slot of the last parity frame
+  bool used[kSlots] = {};
+};
+
 struct DevCtx {
   bool init = false;
   int device = 0;
-  unsigned epoch = 0;   // carry-in tag of the last parity frame
   hipStream_t side = nullptr;   // phase C's side stream
   hipEvent_t fork = nullptr, join = nullptr;
   int side_blocks = 0, side_lds = 0;
@@ -71,13 +108,8 @@ struct DevCtx {
   hipEvent_t ev[kEvSets][5] = {};
   int prof_active = 0, prof_calls = 0, prof_parity = 0;
   DevBuf out;          // rc_render output pixmap
-  DevBuf zcount;       // zero-normalize counter
-  DevBuf scene;        // uploaded packed scene
-  const void* scene_src = nullptr;   // host image last uploaded
-  // parity workspace
-  DevBuf cls, wcarry, deprec, rows, dep_pix, seg_key, seg_start,
-      seg_order, batch_state,
-      cin, counters, team, trace;
+  FrameBufs fb;        // scene, counter and parity workspace of the plain path
+  Pipe pipe;
   int resident_blocks = 0;
   int resident_lds = -1;
   size_t parity_pixels = 0;
@@ -100,7 +132,7 @@ int ctx_get(int device, DevCtx** out) {
     HIP_TRY(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
     for (auto& set : c.ev)
       for (auto& e : set) HIP_TRY(hipEventCreate(&e));
-    if (c.zcount.ensure(64)) return -1;
+    if (c.fb.zcount.ensure(64)) return -1;
     c.device = device;
     c.init = true;
   }
@@ -154,8 +186,11 @@ rc_scene* rc_scene_create(const json_data_t* js) {
 void rc_scene_destroy(rc_scene* s) {
   if (!s) return;
   // forget device copies that were uploaded from this image
-  for (auto& c : g_ctx)
-    if (c.scene_src == s->img) c.scene_src = nullptr;
+  for (auto& c : g_ctx) {
+    if (c.fb.scene_src == s->img) c.fb.scene_src = nullptr;
+    for (auto& f : c.pipe.fb)
+      if (f.scene_src == s->img) f.scene_src = nullptr;
+  }
   std::free(s->img);
   std::free(s);
 }
@@ -166,14 +201,14 @@ int rc_scene_parity_defined(const rc_scene* s) { return s ? s->img->phantom_defi
 
 namespace {
 
-int upload_scene(DevCtx& c, const rc_scene* s, rc::LaunchScene& ls) {
+int upload_scene(FrameBufs& b, hipStream_t stream, const rc_scene* s, rc::LaunchScene& ls) {
   const rc_packed_header* h = s->img;
-  if (c.scene_src != h) {
-    if (c.scene.ensure((size_t)h->bytes)) return -1;
-    HIP_TRY(hipMemcpyAsync(c.scene.p, h, (size_t)h->bytes, hipMemcpyHostToDevice, c.stream));
-    c.scene_src = h;
+  if (b.scene_src != h) {
+    if (b.scene.ensure((size_t)h->bytes)) return -1;
+    HIP_TRY(hipMemcpyAsync(b.scene.p, h, (size_t)h->bytes, hipMemcpyHostToDevice, stream));
+    b.scene_src = h;
   }
-  const char* base = (const char*)c.scene.p;
+  const char* base = (const char*)b.scene.p;
   ls.shapes = (const rc_shape*)(base + h->off_shapes);
   ls.lights = (const rc_light*)(base + h->off_lights);
   ls.pairs = (const rc_shade_pair*)(base + h->off_pairs);
@@ -191,28 +226,29 @@ int upload_scene(DevCtx& c, const rc_scene* s, rc::LaunchScene& ls) {
   return 0;
 }
 
-int ensure_parity(DevCtx& c, int W, int H, rc::ParityWork& w) {
+// res_cus: CUs the resolver grid may occupy (all of them, or the pipeline's partition).
+int ensure_parity(DevCtx& c, FrameBufs& b, int W, int H, rc::ParityWork& w, int res_cus) {
   const size_t P = (size_t)W * H;
-  if (c.cls.ensure(P) || c.wcarry.ensure(P * sizeof(float4)) ||
-      c.deprec.ensure(P * rc::deprec_bytes()) ||
-      c.rows.ensure((size_t)H * (rc::row_stats_bytes() + 2 * sizeof(int) +
+  if (b.cls.ensure(P) || b.wcarry.ensure(P * sizeof(float4)) ||
+      b.deprec.ensure(P * rc::deprec_bytes()) ||
+      b.rows.ensure((size_t)H * (rc::row_stats_bytes() + 2 * sizeof(int) +
                                  2 * sizeof(long long)) + 256) ||
-      c.dep_pix.ensure(P * sizeof(long long)) || c.seg_key.ensure(P * sizeof(long long)) ||
-      c.seg_start.ensure(P * sizeof(int)) ||
-      c.seg_order.ensure((size_t)rc::kSegOrderMax * sizeof(int)) ||
-      c.batch_state.ensure((P / 64 + 2) * sizeof(int)) ||
-      c.counters.ensure(64) || c.team.ensure(rc::team_state_bytes()))
+      b.dep_pix.ensure(P * sizeof(long long)) || b.seg_key.ensure(P * sizeof(long long)) ||
+      b.seg_start.ensure(P * sizeof(int)) ||
+      b.seg_order.ensure((size_t)rc::kSegOrderMax * sizeof(int)) ||
+      b.batch_state.ensure((P / 64 + 2) * sizeof(int)) ||
+      b.counters.ensure(64) || b.team.ensure(rc::team_state_bytes()))
     return -1;
   if (P >= (size_t)1 << 31) return -1;   // DEP indices are 32-bit
   // carry-ins are tagged with a per-frame epoch: a fresh buffer starts at tag 0, which no
   // frame uses
-  if (c.cin.bytes < P * rc::kCinBytes) {
-    if (c.cin.ensure(P * rc::kCinBytes) || hipMemset(c.cin.p, 0, P * rc::kCinBytes) != hipSuccess)
+  if (b.cin.bytes < P * rc::kCinBytes) {
+    if (b.cin.ensure(P * rc::kCinBytes) || hipMemset(b.cin.p, 0, P * rc::kCinBytes) != hipSuccess)
       return -1;
   }
-  if (++c.epoch == 0) {   // wrapped: clear old tags once
-    if (hipMemset(c.cin.p, 0, c.cin.bytes) != hipSuccess) return -1;
-    c.epoch = 1;
+  if (++b.epoch == 0) {   // wrapped: clear old tags once
+    if (hipMemset(b.cin.p, 0, b.cin.bytes) != hipSuccess) return -1;
+    b.epoch = 1;
   }
   const int one_per_cu = std::getenv("RC_RESOLVE_SHARED") ? 0 : 1;
   const int lds = one_per_cu ? 96 * 1024 : 0;
@@ -220,24 +256,29 @@ int ensure_parity(DevCtx& c, int W, int H, rc::ParityWork& w) {
     c.resident_blocks = rc::resolve_blocks_resident(c.cus, lds);
     c.resident_lds = lds;
   }
-  char* r = (char*)c.rows.p;
-  w.cls = (uint8_t*)c.cls.p;
-  w.wcarry = (float4*)c.wcarry.p;
-  w.deprec = c.deprec.p;
+  char* r = (char*)b.rows.p;
+  w.cls = (uint8_t*)b.cls.p;
+  w.wcarry = (float4*)b.wcarry.p;
+  w.deprec = b.deprec.p;
   w.row_prevw = (long long*)r;   r += (size_t)H * sizeof(long long);
   w.row_prevd = (long long*)r;   r += (size_t)H * sizeof(long long);
   w.row_stats = r;               r += (size_t)H * rc::row_stats_bytes();
   w.row_off = (int*)r;           r += (size_t)H * sizeof(int);
   w.row_soff = (int*)r;
-  w.dep_pix = (long long*)c.dep_pix.p;
-  w.seg_key = (long long*)c.seg_key.p;
-  w.seg_start = (int*)c.seg_start.p;
-  w.seg_order = (int*)c.seg_order.p;
-  w.cin = c.cin.p;
-  w.batch_state = (int*)c.batch_state.p;
+  w.dep_pix = (long long*)b.dep_pix.p;
+  w.seg_key = (long long*)b.seg_key.p;
+  w.seg_start = (int*)b.seg_start.p;
+  w.seg_order = (int*)b.seg_order.p;
+  w.cin = b.cin.p;
+  w.batch_state = (int*)b.batch_state.p;
+  const bool piped = res_cus != c.cus;
   w.side = nullptr;
+  w.rstream = nullptr;
+  w.pstream = nullptr;
+  w.rready = w.rdone = w.rt0 = w.rt1 = nullptr;
   w.split_shade = std::getenv("RC_SPLIT_SHADE") ? 1 : 0;
-  if (!std::getenv("RC_NO_SIDE")) {   // phase C overlapped with the resolver
+  if (piped) w.split_shade = 0;   // phase C after the resolver, on the pixel partition
+  if (!piped && !std::getenv("RC_NO_SIDE")) {   // phase C overlapped with the resolver
     if (!c.side) {
       if (hipStreamCreateWithFlags(&c.side, hipStreamNonBlocking) != hipSuccess ||
           hipEventCreateWithFlags(&c.fork, hipEventDisableTiming) != hipSuccess ||
@@ -254,12 +295,12 @@ int ensure_parity(DevCtx& c, int W, int H, rc::ParityWork& w) {
       w.side_lds = c.side_lds;
     }
   }
-  w.epoch = c.epoch;
-  w.counters = (int*)c.counters.p;
-  w.team = c.team.p;
+  w.epoch = b.epoch;
+  w.counters = (int*)b.counters.p;
+  w.team = b.team.p;
   // The team spins on a counter barrier: its blocks (the first of the grid) and the grid as
   // a whole must be co-resident, so the grid never exceeds the resident capacity.
-  w.resolve_blocks = c.resident_blocks;
+  w.resolve_blocks = c.resident_blocks / c.cus * res_cus;   // whole CUs' worth
   w.resolve_lds = c.resident_lds;
   w.team_blocks = std::getenv("RC_TEAM_BLOCKS") ? std::atoi(std::getenv("RC_TEAM_BLOCKS")) : 128;
   if (w.team_blocks > 256) w.team_blocks = 256;
@@ -268,18 +309,18 @@ int ensure_parity(DevCtx& c, int W, int H, rc::ParityWork& w) {
   w.wave_k = std::getenv("RC_WAVE_K") ? std::atoi(std::getenv("RC_WAVE_K")) : 2;
   w.resolve_k = std::getenv("RC_RESOLVE_K") ? std::atoi(std::getenv("RC_RESOLVE_K")) : 1;
   w.coop_group = 0;
-  if (!std::getenv("RC_NO_COOP") && c.scene_src) {
-    const int n = ((const rc_packed_header*)c.scene_src)->n;
+  if (!std::getenv("RC_NO_COOP") && b.scene_src) {
+    const int n = ((const rc_packed_header*)b.scene_src)->n;
     int g = 4;   // groups of >= 4 lanes: the evaluator is specialised for 4, 8 and 16
     while (g < n) g <<= 1;
     if (n >= 1 && g <= 64) w.coop_group = g;
   }
   w.trace = nullptr;
   if (std::getenv("RC_RESOLVE_TRACE")) {
-    if (c.trace.ensure(P * 7 * sizeof(unsigned))) return -1;
-    w.trace = (unsigned*)c.trace.p;
+    if (b.trace.ensure(P * 7 * sizeof(unsigned))) return -1;
+    w.trace = (unsigned*)b.trace.p;
   }
-  w.phase_c_blocks = c.cus * 8;
+  w.phase_c_blocks = (piped ? c.cus - res_cus : c.cus) * 8;
   return 0;
 }
 
@@ -287,8 +328,8 @@ int ensure_parity(DevCtx& c, int W, int H, rc::ParityWork& w) {
 int enqueue_render(DevCtx& c, const rc_scene* s, int W, int H, int row0, int row_step, int nrows,
                    const rc_options* opt, uint8_t* d_out, hipStream_t stream, bool timed) {
   rc::LaunchScene ls;
-  if (upload_scene(c, s, ls)) return -1;
-  unsigned long long* zc = (unsigned long long*)c.zcount.p;
+  if (upload_scene(c.fb, stream, s, ls)) return -1;
+  unsigned long long* zc = (unsigned long long*)c.fb.zcount.p;
   HIP_TRY(hipMemsetAsync(zc, 0, sizeof(unsigned long long), stream));
   const int maxrec = opt->max_recursion;
   const bool parity = opt->mode == RC_MODE_PARITY && maxrec > 1;
@@ -308,8 +349,8 @@ int enqueue_render(DevCtx& c, const rc_scene* s, int W, int H, int row0, int row
     std::fprintf(stderr, "Error: parity mode renders whole images only\n");
     return -1;
   }
-  rc::ParityWork w;
-  if (ensure_parity(c, W, H, w)) {
+  rc::ParityWork w{};
+  if (ensure_parity(c, c.fb, W, H, w, c.cus)) {
     std::fprintf(stderr, "Error: out of device memory for the parity workspace\n");
     return -1;
   }
@@ -319,10 +360,10 @@ int enqueue_render(DevCtx& c, const rc_scene* s, int W, int H, int row0, int row
 
 // After a synchronised parity render: the resolver's and phase C's bounded spins set
 // TeamState.error (first word) if a hand-off never completed; the image is then invalid.
-int check_spin_error(DevCtx& c, const rc_options* opt) {
-  if (!(opt->mode == RC_MODE_PARITY && opt->max_recursion > 1) || !c.team.p) return 0;
+int check_spin_error(FrameBufs& b, const rc_options* opt) {
+  if (!(opt->mode == RC_MODE_PARITY && opt->max_recursion > 1) || !b.team.p) return 0;
   int err = 0;
-  if (hipMemcpy(&err, c.team.p, sizeof err, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  if (hipMemcpy(&err, b.team.p, sizeof err, hipMemcpyDeviceToHost) != hipSuccess) return -1;
   if (err) {
     std::fprintf(stderr, "Error: parity resolver hand-off timed out (code %d)\n", err);
     return -1;
@@ -345,27 +386,27 @@ void fill_device_timing(DevCtx& c, const rc_options* opt, rc_timing* t) {
   t->kernel_ms = k;
   t->resolve_ms = parity ? event_ms(ev[2], ev[3]) : 0.0;
   unsigned long long z = 0;
-  if (hipMemcpy(&z, c.zcount.p, sizeof z, hipMemcpyDeviceToHost) == hipSuccess)
+  if (hipMemcpy(&z, c.fb.zcount.p, sizeof z, hipMemcpyDeviceToHost) == hipSuccess)
     t->zero_normalize = (int64_t)z;
   if (parity) {
     int cnt[4] = {0, 0, 0, 0};
-    if (hipMemcpy(cnt, c.counters.p, sizeof cnt, hipMemcpyDeviceToHost) == hipSuccess)
+    if (hipMemcpy(cnt, c.fb.counters.p, sizeof cnt, hipMemcpyDeviceToHost) == hipSuccess)
       t->dep_pixels = cnt[2];
     if (std::getenv("RC_SIDE_STATS")) {
       int cc[16];
-      if (hipMemcpy(cc, c.counters.p, sizeof cc, hipMemcpyDeviceToHost) == hipSuccess)
+      if (hipMemcpy(cc, c.fb.counters.p, sizeof cc, hipMemcpyDeviceToHost) == hipSuccess)
         std::fprintf(stderr,
                      "side: blocks go %d gave-up %d, tiles side %d finish %d, batches side %d "
                      "finish %d (side_blocks %d)\n",
                      cc[12], cc[13], cc[8], cc[10], cc[9], cc[11], c.side_blocks);
     }
     const char* path = std::getenv("RC_RESOLVE_TRACE");
-    if (path && c.trace.p && cnt[0] > 0) {   // debug: per-segment resolver trace
+    if (path && c.fb.trace.p && cnt[0] > 0) {   // debug: per-segment resolver trace
       std::vector<int> starts(cnt[0]);
       std::vector<unsigned> tr(3 * (size_t)cnt[0]);
-      (void)hipMemcpy(starts.data(), c.seg_start.p, starts.size() * sizeof(int),
+      (void)hipMemcpy(starts.data(), c.fb.seg_start.p, starts.size() * sizeof(int),
                       hipMemcpyDeviceToHost);
-      (void)hipMemcpy(tr.data(), c.trace.p, tr.size() * sizeof(unsigned), hipMemcpyDeviceToHost);
+      (void)hipMemcpy(tr.data(), c.fb.trace.p, tr.size() * sizeof(unsigned), hipMemcpyDeviceToHost);
       if (FILE* f = std::fopen(path, "w")) {
         std::fprintf(f, "# seg start len ticks_100MHz evals(team: rounds|0x80000000) cycles\n");
         for (int k = 0; k < cnt[0]; ++k) {
@@ -378,7 +419,7 @@ void fill_device_timing(DevCtx& c, const rc_options* opt, rc_timing* t) {
       {   // per-segment start times (regular waves)
         std::vector<unsigned> st(cnt[0]);
         (void)hipMemcpy(st.data(),
-                        (const unsigned*)c.trace.p + 3 * (size_t)cnt[2] + 4 * (size_t)cnt[0] +
+                        (const unsigned*)c.fb.trace.p + 3 * (size_t)cnt[2] + 4 * (size_t)cnt[0] +
                             8 * 8192,
                         st.size() * sizeof(unsigned), hipMemcpyDeviceToHost);
         std::string p4 = std::string(path) + ".start";
@@ -390,7 +431,7 @@ void fill_device_timing(DevCtx& c, const rc_options* opt, rc_timing* t) {
       {   // per-round team log (k_resolve, team blocks)
         std::vector<unsigned> tl(8 * 8192);
         (void)hipMemcpy(tl.data(),
-                        (const unsigned*)c.trace.p + 3 * (size_t)cnt[2] + 4 * (size_t)cnt[0],
+                        (const unsigned*)c.fb.trace.p + 3 * (size_t)cnt[2] + 4 * (size_t)cnt[0],
                         tl.size() * sizeof(unsigned), hipMemcpyDeviceToHost);
         std::string p3 = std::string(path) + ".team";
         if (FILE* f = std::fopen(p3.c_str(), "w")) {
@@ -405,7 +446,7 @@ void fill_device_timing(DevCtx& c, const rc_options* opt, rc_timing* t) {
       }
 #if RC_STAMPS
       std::vector<unsigned> sp(4 * (size_t)cnt[0]);
-      (void)hipMemcpy(sp.data(), (const unsigned*)c.trace.p + 3 * (size_t)cnt[2],
+      (void)hipMemcpy(sp.data(), (const unsigned*)c.fb.trace.p + 3 * (size_t)cnt[2],
                       sp.size() * sizeof(unsigned), hipMemcpyDeviceToHost);
       std::string p2 = std::string(path) + ".stamps";
       if (FILE* f = std::fopen(p2.c_str(), "w")) {
@@ -447,11 +488,168 @@ int rc_render_device(const rc_scene* s, int W, int H, int row0, int row_step, in
   if (timing) {
     std::memset(timing, 0, sizeof *timing);
     HIP_TRY(hipStreamSynchronize(st));
-    if (check_spin_error(*c, opt)) return -1;
+    if (check_spin_error(c->fb, opt)) return -1;
     fill_device_timing(*c, opt, timing);
     timing->total_ms = timing->kernel_ms;
   }
   return 0;
+}
+
+// ------------------------------------------------------------ pipelined frames --
+}  // extern "C"
+
+namespace {
+
+// Release the pipelines' CU-masked streams and events before the runtime's own teardown
+// (left to process exit they crash a profiled process's finalisation).
+void pipe_release_all() {
+  for (auto& c : g_ctx) {
+    Pipe& p = c.pipe;
+    if (!p.init) continue;
+    (void)hipSetDevice(c.device);
+    (void)hipDeviceSynchronize();
+    for (int k = 0; k < Pipe::kSlots; ++k) {
+      (void)hipStreamDestroy(p.pix[k]);
+      (void)hipEventDestroy(p.ready[k]);
+      (void)hipEventDestroy(p.done[k]);
+    }
+    for (int r = 0; r < Pipe::kLanes; ++r) (void)hipStreamDestroy(p.res[r]);
+    for (auto& e : p.rt) {
+      (void)hipEventDestroy(e[0]);
+      (void)hipEventDestroy(e[1]);
+    }
+    p.init = false;
+  }
+}
+
+int pipe_init(DevCtx& c) {
+  Pipe& p = c.pipe;
+  if (p.init) return 0;
+  static bool registered = false;
+  if (!registered) {
+    std::atexit(pipe_release_all);
+    registered = true;
+  }
+  // partition A: the low `res` bits of the CU mask, which the driver deals round-robin over
+  // the XCDs (bit i -> XCD i mod 8), so both partitions span every XCD.
+  int res = c.cus / 2;
+  if (const char* e = std::getenv("RC_PIPE_RES_CUS")) res = std::atoi(e);
+  if (const char* e = std::getenv("RC_PIPE_RESOLVERS")) p.lanes = std::atoi(e);
+  if (p.lanes < 1) p.lanes = 1;
+  if (p.lanes > Pipe::kLanes) p.lanes = Pipe::kLanes;
+  res = res / (8 * p.lanes) * (8 * p.lanes);   // whole CUs per XCD for every resolver
+  if (res < 16 * p.lanes) res = 16 * p.lanes;
+  if (res > c.cus - 16) res = (c.cus - 16) / (8 * p.lanes) * (8 * p.lanes);
+  const int words = (c.cus + 31) / 32;
+  std::vector<uint32_t> ma(words, 0), mb(words, 0);
+  for (int i = 0; i < c.cus; ++i) (i < res ? ma : mb)[i / 32] |= 1u << (i % 32);
+  for (int r = 0; r < Pipe::kLanes; ++r)
+    HIP_TRY(hipExtStreamCreateWithCUMask(&p.res[r], (uint32_t)words, ma.data()));
+  for (int k = 0; k < Pipe::kSlots; ++k) {
+    HIP_TRY(hipExtStreamCreateWithCUMask(&p.pix[k], (uint32_t)words, mb.data()));
+    HIP_TRY(hipEventCreateWithFlags(&p.ready[k], hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&p.done[k], hipEventDisableTiming));
+  }
+  for (auto& e : p.rt) {
+    HIP_TRY(hipEventCreate(&e[0]));
+    HIP_TRY(hipEventCreate(&e[1]));
+  }
+  p.res_cus = res;
+  p.init = true;
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rc_frame_submit(const rc_scene* s, int W, int H, const rc_options* opt, uint8_t* d_out) {
+  if (!s || !opt || !d_out || W <= 0 || H <= 0) return -1;
+  int dev = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  DevCtx* c;
+  if (ctx_get(dev, &c)) return -1;
+  const int maxrec = opt->max_recursion;
+  if (!(opt->mode == RC_MODE_PARITY && maxrec > 1)) {   // no serial stage: whole GPU, in order
+    if (enqueue_render(*c, s, W, H, 0, 1, H, opt, d_out, c->stream, false)) return -1;
+    c->pipe.frames++;
+    return 0;
+  }
+  if (pipe_init(*c)) return -1;
+  Pipe& p = c->pipe;
+  const int k = (int)(p.total % Pipe::kSlots);
+  const int lane = (int)(p.total % p.lanes);
+  FrameBufs& b = p.fb[k];
+  // A frame submitted into an empty pipeline has no resolver to hide behind: its phase A
+  // and compaction take the whole device (then phase C returns to the slot's partition).
+  // Slot k's previous frame is complete (rc_frames_wait synchronised every slot).
+  const bool first = p.submitted == 0;
+  hipStream_t st = first ? c->stream : p.pix[k];
+  rc::LaunchScene ls;
+  if (upload_scene(b, st, s, ls) || b.zcount.ensure(64)) return -1;
+  unsigned long long* zc = (unsigned long long*)b.zcount.p;
+  HIP_TRY(hipMemsetAsync(zc, 0, sizeof(unsigned long long), st));
+  rc::ParityWork w{};
+  if (ensure_parity(*c, b, W, H, w, p.res_cus / p.lanes)) {
+    std::fprintf(stderr, "Error: out of device memory for the parity workspace\n");
+    return -1;
+  }
+  w.rstream = p.res[lane];
+  w.pstream = first ? p.pix[k] : nullptr;
+  w.rready = p.ready[k];
+  w.rdone = p.done[k];
+  const int e = (int)(p.submitted % Pipe::kEv);
+  w.rt0 = p.rt[e][0];
+  w.rt1 = p.rt[e][1];
+  HIP_TRY(rc::launch_parity(ls, W, H, maxrec, d_out, w, zc, st, nullptr));
+  p.submitted++;
+  p.frames++;
+  p.total++;
+  p.last = k;
+  p.used[k] = true;
+  return 0;
+}
+
+int rc_frames_wait(rc_timing* timing) {
+  int dev = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  DevCtx* c;
+  if (ctx_get(dev, &c)) return -1;
+  Pipe& p = c->pipe;
+  if (timing) std::memset(timing, 0, sizeof *timing);
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  int rc = 0;
+  if (p.init) {
+    for (int k = 0; k < Pipe::kSlots; ++k) HIP_TRY(hipStreamSynchronize(p.pix[k]));
+    for (int r = 0; r < Pipe::kLanes; ++r) HIP_TRY(hipStreamSynchronize(p.res[r]));
+    for (int k = 0; k < Pipe::kSlots; ++k) {   // the last frame of each slot
+      if (!p.used[k] || !p.fb[k].team.p) continue;
+      int err = 0;
+      HIP_TRY(hipMemcpy(&err, p.fb[k].team.p, sizeof err, hipMemcpyDeviceToHost));
+      if (err) {
+        std::fprintf(stderr, "Error: parity resolver hand-off timed out (code %d)\n", err);
+        rc = -1;
+      }
+    }
+    const int n = p.submitted < Pipe::kEv ? (int)p.submitted : Pipe::kEv;
+    double sum = 0.0;
+    for (int e = 0; e < n; ++e) sum += event_ms(p.rt[e][0], p.rt[e][1]);
+    if (n > 0) g_last_kernel_ms = sum / n;
+    if (timing && n > 0 && p.last >= 0) {
+      timing->resolve_ms = sum / n;
+      FrameBufs& b = p.fb[p.last];
+      int cnt[4] = {0, 0, 0, 0};
+      if (b.counters.p &&
+          hipMemcpy(cnt, b.counters.p, sizeof cnt, hipMemcpyDeviceToHost) == hipSuccess)
+        timing->dep_pixels = cnt[2];
+      unsigned long long z = 0;
+      if (hipMemcpy(&z, b.zcount.p, sizeof z, hipMemcpyDeviceToHost) == hipSuccess)
+        timing->zero_normalize = (int64_t)z;
+    }
+  }
+  p.frames = 0;
+  p.submitted = 0;
+  return rc;
 }
 
 int rc_profile_begin(void) {
@@ -546,7 +744,7 @@ int rc_render(const rc_scene* s, int W, int H, const rc_options* opt, uint8_t* p
       rcodes[g] = -1;
       return;
     }
-    if (check_spin_error(*c, opt)) {
+    if (check_spin_error(c->fb, opt)) {
       rcodes[g] = -1;
       return;
     }

@@ -36,6 +36,11 @@ struct Scene {
   const rc_shape* __restrict__ shapes;   // n + 1 records (n = phantom)
   const rc_light* __restrict__ lights;   // m records
   const rc_shade_pair* __restrict__ pairs;
+  // Per-lane (divergent) record reads — the winner's frame, its shading record and colour
+  // pairs — go through these: LDS copies when the kernel staged the scene (stage_scene),
+  // else the global records.  Uniform loops over shapes/lights keep the scalar path above.
+  const rc_shape* lshapes;
+  const rc_shade_pair* lpairs;
   int n, m;
   unsigned long long refl_mask;          // bit k: shape k has reflectivity > 0 (k < 64)
   int has_quadric;                       // any quadric: picks the evaluator specialisation
@@ -44,7 +49,7 @@ struct Scene {
 // refl[obj] > 0 (C/raycast.c:352) from a register bitmask when n <= 64
 __device__ __forceinline__ bool reflective(const Scene& sc, int obj) {
   if (sc.n <= 64) return (sc.refl_mask >> obj) & 1ull;
-  return sc.shapes[obj].refl > 0.0f;
+  return sc.lshapes[obj].refl > 0.0f;
 }
 
 struct Cam {
@@ -331,7 +336,7 @@ __device__ __forceinline__ bool shadowed(const Scene& sc, V3 O, V3 D, int skip) 
 __device__ __forceinline__ void hit_frame(const Scene& sc, int idx, V3 O, V3 D, float t, V3& P,
                                           V3& N, int& zero_events) {
   P = v3(O.x + D.x * t, O.y + D.y * t, O.z + D.z * t);
-  const rc_shape& s = sc.shapes[idx];
+  const rc_shape& s = sc.lshapes[idx];
   const int type = s.type;
   if (type == RC_SHAPE_SPHERE) {
     const float inv = s.inv_r;
@@ -359,12 +364,12 @@ __device__ __forceinline__ void hit_frame(const Scene& sc, int idx, V3 O, V3 D, 
 
 // calc_color (C/raycast.c:381-421) for shape `idx` (sc.n = the phantom shapes_list[-1]).
 __device__ __forceinline__ V3 shade(const Scene& sc, int idx, V3 P, V3 N, V3 D, int& zero_events) {
-  const rc_shape& o = sc.shapes[idx];
+  const rc_shape& o = sc.lshapes[idx];
   const float opacity = o.opacity;
   V3 out = v3(0.0f, 0.0f, 0.0f);
   if (!(opacity > 0.0f)) return out;
   const int skip = (idx == sc.n) ? -1 : idx;
-  const rc_shade_pair* pr = sc.pairs + (size_t)idx * sc.m;
+  const rc_shade_pair* pr = sc.lpairs + (size_t)idx * sc.m;
   for (int l = 0; l < sc.m; ++l) {
     const rc_light& L = sc.lights[l];
     V3 ld = v3(L.pos[0] - P.x, L.pos[1] - P.y, L.pos[2] - P.z);
@@ -375,11 +380,16 @@ __device__ __forceinline__ V3 shade(const Scene& sc, int idx, V3 P, V3 N, V3 D, 
     const float lin = L.r0 + L.r1 * dist;
     const float rad =
         (float)(1.0 / ((double)lin + (double)L.r2 * ((double)dist * (double)dist)));
-    // angular attenuation C/raycast.c:679-696
+    // angular attenuation C/raycast.c:679-696.  v = normalize(P - L.pos): P - L.pos is -ld
+    // component for component (round-to-nearest is sign-symmetric), so v = -ld and
+    // alpha = -dot(ld, dir) exactly.  A zero-length ld (P on the light) is +0 in every
+    // component either way: then v = ld, and the reference counts a second zero event.
     float ang = 1.0f;
     if (L.type == RC_LIGHT_SPOT) {
-      V3 v = normalize(v3(P.x - L.pos[0], P.y - L.pos[1], P.z - L.pos[2]), zero_events);
-      const float alpha = dot(v, v3(L.dir[0], L.dir[1], L.dir[2]));
+      const float a = dot(ld, v3(L.dir[0], L.dir[1], L.dir[2]));
+      const bool z = dist == 0.0f;
+      zero_events += z ? 1 : 0;
+      const float alpha = z ? a : -a;
       if (alpha < L.cos_theta) {
         ang = 0.0f;
       } else if (L.a0_kind == RC_A0_INT) {
@@ -469,11 +479,11 @@ __device__ __forceinline__ void shoot(const Scene& sc, V3 d, int maxrec, V3 carr
 
   int obj = i0, S = i0;
   V3 O = P0, D = d, N = N0, C = carry;
-  float T = sc.shapes[i0].refl;
+  float T = sc.lshapes[i0].refl;
   V3 out = v3(0.0f, 0.0f, 0.0f);
   bool wrote = false;
   for (int lvl = 1; lvl < maxrec; ++lvl) {              // C/raycast.c:348-376
-    if (!(sc.shapes[obj].refl > 0.0f)) break;
+    if (!reflective(sc, obj)) break;
     D = normalize(reflect(D, N), zero_events);
     float t;
     const int i = nearest(sc, O, D, S, t);
@@ -496,7 +506,7 @@ __device__ __forceinline__ void shoot(const Scene& sc, V3 d, int maxrec, V3 carr
       out.x = out.x + col.x * T;
       out.y = out.y + col.y * T;
       out.z = out.z + col.z * T;
-      T = T * sc.shapes[obj].refl;
+      T = T * sc.lshapes[obj].refl;
     }
     O = C;
     S = i;
@@ -517,7 +527,7 @@ __device__ __forceinline__ V3 carry_path(const Scene& sc, const DepRec& r, int m
   V3 D = v3(r.ax, r.ay, r.az), N = v3(r.n0x, r.n0y, r.n0z), C = c;   // level 2's direction
   int obj = r.obj0, S = -1;
   for (int lvl = 2; lvl < maxrec; ++lvl) {
-    if (!(sc.shapes[obj].refl > 0.0f)) break;
+    if (!reflective(sc, obj)) break;
     if (lvl > 2) D = normalize(reflect(D, N), zero_events);
     float t;
     const int i = nearest(sc, C, D, S, t);

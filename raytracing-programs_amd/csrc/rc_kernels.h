@@ -53,6 +53,12 @@ struct ParityWork {
   int resolve_k;            // the same for the team leader's block window
   int coop_group;           // lanes per entry of the cooperative evaluator (0: off)
   unsigned* trace;          // optional [2*nseg] per-segment {ticks, evals} (debug)
+  // Pipelined frames (rc_frame_submit): the resolver runs on its own stream (a CU partition
+  // of its own) between two hand-off events; null rstream = everything on the main stream.
+  hipStream_t rstream;
+  hipStream_t pstream;      // phase C's stream (null: the main stream)
+  hipEvent_t rready, rdone; // main -> rstream after compaction; rstream -> pstream after it
+  hipEvent_t rt0, rt1;      // optional: resolver start / end on rstream
 };
 
 constexpr int kSegOrderMax = 65536;   // segments ordered for the resolver queue (else FIFO)

@@ -50,11 +50,49 @@ __device__ __forceinline__ void flush_events(int zero_events, unsigned long long
   if (zero_events) atomicAdd(counter, (unsigned long long)zero_events);
 }
 
+// The pixel kernels' divergent record reads (the winner's frame, shading record and colour
+// pairs: Scene::lshapes / lpairs) come from an LDS copy of the scene when it is small
+// enough: an LDS read instead of a vector-memory round trip per lane.  The
+// uniform loops over shapes and lights keep their scalar loads.
+constexpr int kStageShapes = 32;   // shape records, phantom included
+constexpr int kStagePairs = 128;   // (shape, light) colour pairs
+struct SceneStage {
+  rc_shape shapes[kStageShapes];
+  rc_shade_pair pairs[kStagePairs];
+};
+template <bool kStage>
+struct StageBuf {
+  SceneStage s;
+};
+template <>
+struct StageBuf<false> {
+  int unused;
+};
+
+// Every thread of the workgroup must call this (it has a barrier).
+template <bool kStage>
+__device__ __forceinline__ void stage_scene(Scene& sc, StageBuf<kStage>& buf) {
+  if constexpr (kStage) {
+    const int ws = (int)(sizeof(rc_shape) / 4) * (sc.n + 1);
+    for (int i = threadIdx.x; i < ws; i += blockDim.x)
+      ((unsigned*)buf.s.shapes)[i] = ((const unsigned*)sc.shapes)[i];
+    const int wp = (int)(sizeof(rc_shade_pair) / 4) * (sc.n + 1) * sc.m;
+    for (int i = threadIdx.x; i < wp; i += blockDim.x)
+      ((unsigned*)buf.s.pairs)[i] = ((const unsigned*)sc.pairs)[i];
+    __syncthreads();
+    sc.lshapes = buf.s.shapes;
+    sc.lpairs = buf.s.pairs;
+  }
+}
+
 // ------------------------------------------------------------------ fast / depth 0 --
+template <bool kStage>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_PHASE_A_WAVES))) k_render(Scene sc, Cam cam, int W, int H, int row0,
                                                    int row_step, int nrows, int maxrec,
                                                    uint8_t* __restrict__ out,
                                                    unsigned long long* __restrict__ zcount) {
+  __shared__ StageBuf<kStage> stage;
+  stage_scene<kStage>(sc, stage);
   int lx, ly;
   tile_pixel(lx, ly);
   const int x = blockIdx.x * kTile + lx;
@@ -70,12 +108,15 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_
 }
 
 // ------------------------------------------------------------------ parity phase A --
+template <bool kStage>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_PHASE_A_WAVES))) k_phase_a(Scene sc, Cam cam, int W, int H, int maxrec,
                                                     uint8_t* __restrict__ out,
                                                     uint8_t* __restrict__ cls,
                                                     float4* __restrict__ wcarry,
                                                     DepRec* __restrict__ deprec,
                                                     unsigned long long* __restrict__ zcount) {
+  __shared__ StageBuf<kStage> stage;
+  stage_scene<kStage>(sc, stage);
   int lx, ly;
   tile_pixel(lx, ly);
   const int x = blockIdx.x * kTile + lx;
@@ -97,10 +138,13 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_
 }
 
 // Phase A's carry part only (no shading): k_side shades the non-DEP pixels off the critical path.
+template <bool kStage>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_PHASE_A_WAVES))) k_classify(Scene sc, Cam cam, int W, int H, int maxrec,
                                                      uint8_t* __restrict__ cls,
                                                      float4* __restrict__ wcarry,
                                                      DepRec* __restrict__ deprec) {
+  __shared__ StageBuf<kStage> stage;
+  stage_scene<kStage>(sc, stage);
   int lx, ly;
   tile_pixel(lx, ly);
   const int x = blockIdx.x * kTile + lx;
@@ -729,6 +773,7 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
       ((unsigned*)s_shapes)[i] = ((const unsigned*)sc.shapes)[i];
     __syncthreads();
     sc.shapes = s_shapes;
+    sc.lshapes = s_shapes;
   }
 #if RC_STAMPS
   Stamps stp = {{0, 0, 0, 0}, 0};
@@ -1052,6 +1097,7 @@ __device__ __forceinline__ void phase_c_passes(const Scene& sc, const Cam& cam, 
   }
 }
 
+template <bool kStage>
 __global__ void __launch_bounds__(kSideBlock) k_side(
     Scene sc, Cam cam, int W, int H, int maxrec, const uint8_t* __restrict__ cls,
     const long long* __restrict__ dep_pix, CinG* __restrict__ cin, int* __restrict__ counters,
@@ -1059,6 +1105,8 @@ __global__ void __launch_bounds__(kSideBlock) k_side(
     unsigned long long* __restrict__ zcount, TeamState* __restrict__ ts, int resolve_blocks,
     unsigned tag, int tiles) {
   __shared__ int s_go;
+  __shared__ StageBuf<kStage> stage;
+  stage_scene<kStage>(sc, stage);
   // The grid is sized so that a resolver workgroup always fits beside k_side's workgroups on
   // a CU (phase_c_side_blocks), so waiting here for every resolver workgroup to be resident
   // cannot hold one out; the wait is bounded anyway (20 ms, then this workgroup leaves its
@@ -1093,12 +1141,15 @@ __global__ void __launch_bounds__(kSideBlock) k_side(
 }
 
 // After the resolver: the tiles (when `tiles`) and DEP batches k_side has not claimed.
+template <bool kStage>
 __global__ void __launch_bounds__(kBlock) k_finish(
     Scene sc, Cam cam, int W, int H, int maxrec, const uint8_t* __restrict__ cls,
     const long long* __restrict__ dep_pix, CinG* __restrict__ cin, int* __restrict__ counters,
     int* __restrict__ batch_state, uint8_t* __restrict__ out,
     unsigned long long* __restrict__ zcount, TeamState* __restrict__ ts, unsigned tag,
     int tiles) {
+  __shared__ StageBuf<kStage> stage;
+  stage_scene<kStage>(sc, stage);
   int zero = 0;
   const int ntiles = ((W + 7) >> 3) * ((H + 7) >> 3);
   while (tiles) {
@@ -1118,11 +1169,16 @@ static Scene make_scene(const LaunchScene& s) {
   sc.shapes = s.shapes;
   sc.lights = s.lights;
   sc.pairs = s.pairs;
+  sc.lshapes = s.shapes;
+  sc.lpairs = s.pairs;
   sc.n = s.n;
   sc.m = s.m;
   sc.refl_mask = s.refl_mask;
   sc.has_quadric = s.has_quadric;
   return sc;
+}
+static bool stage_fits(const LaunchScene& s) {
+  return s.n + 1 <= kStageShapes && (s.n + 1) * s.m <= kStagePairs;
 }
 static Cam make_cam(const LaunchScene& s, int W, int H) {
   Cam c;
@@ -1137,7 +1193,7 @@ hipError_t launch_render(const LaunchScene& s, int W, int H, int row0, int row_s
                          int maxrec, uint8_t* out, unsigned long long* zcount,
                          hipStream_t stream) {
   dim3 grid((W + kTile - 1) / kTile, (nrows + kTile - 1) / kTile);
-  hipLaunchKernelGGL(k_render, grid, dim3(kBlock), 0, stream, make_scene(s), make_cam(s, W, H),
+  hipLaunchKernelGGL(stage_fits(s) ? k_render<true> : k_render<false>, grid, dim3(kBlock), 0, stream, make_scene(s), make_cam(s, W, H),
                      W, H, row0, row_step, nrows, maxrec, out, zcount);
   return hipGetLastError();
 }
@@ -1149,12 +1205,13 @@ hipError_t launch_parity(const LaunchScene& s, int W, int H, int maxrec, uint8_t
   // [3] after phase C
   const Scene sc = make_scene(s);
   const Cam cam = make_cam(s, W, H);
+  const bool st = stage_fits(s);
   dim3 grid((W + kTile - 1) / kTile, (H + kTile - 1) / kTile);
   if (w.side && w.split_shade)   // carry part only; colours shaded beside the resolver (k_side)
-    hipLaunchKernelGGL(k_classify, grid, dim3(kBlock), 0, stream, sc, cam, W, H, maxrec, w.cls,
+    hipLaunchKernelGGL(st ? k_classify<true> : k_classify<false>, grid, dim3(kBlock), 0, stream, sc, cam, W, H, maxrec, w.cls,
                        w.wcarry, (DepRec*)w.deprec);
   else
-    hipLaunchKernelGGL(k_phase_a, grid, dim3(kBlock), 0, stream, sc, cam, W, H, maxrec, out,
+    hipLaunchKernelGGL(st ? k_phase_a<true> : k_phase_a<false>, grid, dim3(kBlock), 0, stream, sc, cam, W, H, maxrec, out,
                        w.cls, w.wcarry, (DepRec*)w.deprec, zcount);
   if (ev) (void)hipEventRecord(ev[0], stream);
   (void)hipMemsetAsync(w.counters, 0, 16 * sizeof(int), stream);   // nseg, head, ndep, ...
@@ -1173,22 +1230,35 @@ hipError_t launch_parity(const LaunchScene& s, int W, int H, int maxrec, uint8_t
   // steps are latency-bound, so a resolver wave should not share its SIMD
   if (ev) (void)hipEventRecord(ev[1], stream);
   if (w.side) (void)hipEventRecord(w.fork, stream);
+  hipStream_t rs = stream;
+  if (w.rstream) {   // pipelined: the resolver on its partition, in frame order
+    rs = w.rstream;
+    (void)hipEventRecord(w.rready, stream);
+    (void)hipStreamWaitEvent(rs, w.rready, 0);
+    if (w.rt0) (void)hipEventRecord(w.rt0, rs);
+  }
   auto kres = s.n <= kLdsShapes ? k_resolve<true> : k_resolve<false>;
-  hipLaunchKernelGGL(kres, dim3(w.resolve_blocks), dim3(kResolveBlock), w.resolve_lds, stream, sc,
+  hipLaunchKernelGGL(kres, dim3(w.resolve_blocks), dim3(kResolveBlock), w.resolve_lds, rs, sc,
                      maxrec, (const DepRec*)w.deprec, w.dep_pix, w.seg_key, w.wcarry,
                      w.seg_start, w.seg_order, w.counters, w.counters + 1, (CinG*)w.cin, w.team_blocks,
                      w.long_len, (TeamState*)w.team, w.trace, w.coop_group, w.wave_k,
                      w.resolve_k, w.epoch);
+  if (w.rstream) {
+    if (w.rt1) (void)hipEventRecord(w.rt1, rs);
+    (void)hipEventRecord(w.rdone, rs);
+    if (w.pstream) stream = w.pstream;
+    (void)hipStreamWaitEvent(stream, w.rdone, 0);
+  }
   if (w.side) {   // colours and phase C beside the resolver
     (void)hipStreamWaitEvent(w.side, w.fork, 0);
-    hipLaunchKernelGGL(k_side, dim3(w.side_blocks), dim3(kSideBlock), w.side_lds, w.side, sc, cam,
+    hipLaunchKernelGGL(st ? k_side<true> : k_side<false>, dim3(w.side_blocks), dim3(kSideBlock), w.side_lds, w.side, sc, cam,
                        W, H, maxrec, w.cls, w.dep_pix, (CinG*)w.cin, w.counters, w.batch_state,
                        out, zcount, (TeamState*)w.team, w.resolve_blocks, w.epoch,
                        w.split_shade);
     (void)hipEventRecord(w.join, w.side);
   }
   if (ev) (void)hipEventRecord(ev[2], stream);
-  hipLaunchKernelGGL(k_finish, dim3(w.phase_c_blocks), dim3(kBlock), 0, stream, sc, cam, W, H,
+  hipLaunchKernelGGL(st ? k_finish<true> : k_finish<false>, dim3(w.phase_c_blocks), dim3(kBlock), 0, stream, sc, cam, W, H,
                      maxrec, w.cls, w.dep_pix, (CinG*)w.cin, w.counters, w.batch_state, out,
                      zcount, (TeamState*)w.team, w.epoch, (w.side && w.split_shade) ? 1 : 0);
   if (w.side) (void)hipStreamWaitEvent(stream, w.join, 0);
@@ -1219,10 +1289,12 @@ int side_lds_bytes(int resolve_dyn_lds) {
 }
 
 int phase_c_side_blocks(int cus, int side_lds) {
-  (void)hipFuncSetAttribute((const void*)k_side, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            side_lds);
-  int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_side, kSideBlock, side_lds) !=
+  (void)hipFuncSetAttribute((const void*)k_side<false>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, side_lds);
+  (void)hipFuncSetAttribute((const void*)k_side<true>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, side_lds);
+  int per_cu = 0;   // the staged variant (more LDS) bounds both
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_side<true>, kSideBlock, side_lds) !=
           hipSuccess ||
       per_cu <= 0)
     per_cu = 1;

@@ -153,3 +153,32 @@ def test_device_render_matches_host(scenes, table):
     torch.cuda.synchronize()
     full = rc.render(scenes["quadric"], 512, 512, depth=6, mode="fast")
     np.testing.assert_array_equal(sh.cpu().numpy(), full[1::3])
+
+
+def test_frames_in_flight(scenes, table):
+    """rc_frame_submit: consecutive frames overlap on two CU partitions (the resolver of one
+    beside the pixel phases of the next); every frame is still byte-identical.  Mixed scenes,
+    sizes and modes exercise the slot workspaces' re-use and re-upload."""
+    torch = pytest.importorskip("torch")
+    seq = ["quadric:4096x4096:d6:parity", "reflection:2048x2048:d4:parity",
+           "quadric:4096x4096:d6:parity", "simple:1024x1024:d6:parity",
+           "quadric:1024x1024:d6:fast", "quadric:512x384:d6:parity",
+           "quadric:4096x4096:d6:parity", "quadric:4096x4096:d6:parity"]
+    jobs = []
+    for key in seq:
+        scene, size, d, mode = key.split(":")
+        w, h = map(int, size.split("x"))
+        jobs.append((key, scene, w, h, int(d[1:]), mode,
+                     torch.empty((h, w, 3), dtype=torch.uint8, device="cuda")))
+    torch.cuda.synchronize()
+    for _ in range(2):   # a second round re-uses both slots' workspaces
+        for key, scene, w, h, d, mode, buf in jobs:
+            buf.zero_()
+        torch.cuda.synchronize()
+        for key, scene, w, h, d, mode, buf in jobs:
+            rc.frame_submit(scenes[scene], w, h, buf.data_ptr(), depth=d, mode=mode)
+        tim = {}
+        rc.frames_wait(tim)
+        assert tim["resolve_ms"] > 0.0
+        for key, scene, w, h, d, mode, buf in jobs:
+            assert p3_md5(buf.cpu().numpy()) == table[key]["md5"], key
