@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 
 #include <chrono>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -223,6 +224,12 @@ int upload_scene(FrameBufs& b, hipStream_t stream, const rc_scene* s, rc::Launch
     if (hs[k].refl > 0.0f) ls.refl_mask |= 1ull << k;
   for (int k = 0; k < h->n; ++k)
     if (hs[k].type == RC_SHAPE_QUADRIC) ls.has_quadric = 1;
+  // Clean DEP entries' colour = phase A's primary shade exactly when every bounce level's
+  // shade of them is zero: the phantom (shapes_list[-1], index n) is black, and the
+  // reflectivity product T stays finite (0 * T == 0).
+  ls.dep_fast = !(hs[h->n].opacity > 0.0f) && !std::getenv("RC_NO_DEP_FAST");
+  for (int k = 0; k < h->n; ++k)
+    if (!(std::fabs(hs[k].refl) < 1.0e5f)) ls.dep_fast = 0;
   return 0;
 }
 
@@ -246,7 +253,7 @@ int ensure_parity(DevCtx& c, FrameBufs& b, int W, int H, rc::ParityWork& w, int 
     if (b.cin.ensure(P * rc::kCinBytes) || hipMemset(b.cin.p, 0, P * rc::kCinBytes) != hipSuccess)
       return -1;
   }
-  if (++b.epoch == 0) {   // wrapped: clear old tags once
+  if (++b.epoch >= 0x80000000u) {   // wrapped (tags keep bit 31 for a flag): clear once
     if (hipMemset(b.cin.p, 0, b.cin.bytes) != hipSuccess) return -1;
     b.epoch = 1;
   }
@@ -354,6 +361,7 @@ int enqueue_render(DevCtx& c, const rc_scene* s, int W, int H, int row0, int row
     std::fprintf(stderr, "Error: out of device memory for the parity workspace\n");
     return -1;
   }
+  if (w.split_shade) ls.dep_fast = 0;   // k_classify leaves no primary shade
   HIP_TRY(rc::launch_parity(ls, W, H, maxrec, d_out, w, zc, stream, timed ? ev + 1 : nullptr));
   return 0;
 }

@@ -44,6 +44,10 @@ struct Scene {
   int n, m;
   unsigned long long refl_mask;          // bit k: shape k has reflectivity > 0 (k < 64)
   int has_quadric;                       // any quadric: picks the evaluator specialisation
+  // Clean DEP entries (no bounce level hits at their carry-in) take their colour from phase
+  // A's primary shade: set when every level's shade of such an entry is exactly zero (black
+  // phantom, finite reflectivities; host check in upload_scene).
+  int dep_fast;
 };
 
 // refl[obj] > 0 (C/raycast.c:352) from a register bitmask when n <= 64
@@ -459,6 +463,7 @@ struct PixelOut {
   uint8_t cls;
   V3 carry;     // carry-out for writers (last bounce-hit point)
   DepRec dep;
+  V3 pcol;      // DEP pixels under dep_fast: the primary shade (C/raycast.c:377)
 };
 
 // iterative_shoot (C/raycast.c:315-379) for one pixel under MODE.
@@ -466,16 +471,19 @@ struct PixelOut {
 //  kModeParityA  : a miss at level 1 stops here (cls = DEP, dep record filled).
 //  kModeParityC  : `carry` is this pixel's scan-order carry-in.
 //  kModeClassify : kModeParityA's control flow and carry without any shading (rgb = 0).
+// Under sc.dep_fast phase A also shades a DEP pixel's primary hit (po.pcol) and counts the
+// events of everything it computed for it (phase C resumes at level 2: shade_dep_cont).
 template <int MODE>
 __device__ __forceinline__ void shoot(const Scene& sc, V3 d, int maxrec, V3 carry, PixelOut& po,
                                       int& zero_events) {
   po.rgb = v3(0.0f, 0.0f, 0.0f);
   po.cls = kClsIdent;
+  int zp = 0;   // events of the primary part (a DEP pixel's share of phase A)
   float t0;
   const int i0 = nearest(sc, v3(0.0f, 0.0f, 0.0f), d, -1, t0);
   if (i0 < 0) return;                                   // C/raycast.c:328-331
   V3 P0, N0;
-  hit_frame(sc, i0, v3(0.0f, 0.0f, 0.0f), d, t0, P0, N0, zero_events);
+  hit_frame(sc, i0, v3(0.0f, 0.0f, 0.0f), d, t0, P0, N0, zp);
 
   int obj = i0, S = i0;
   V3 O = P0, D = d, N = N0, C = carry;
@@ -484,7 +492,10 @@ __device__ __forceinline__ void shoot(const Scene& sc, V3 d, int maxrec, V3 carr
   bool wrote = false;
   for (int lvl = 1; lvl < maxrec; ++lvl) {              // C/raycast.c:348-376
     if (!reflective(sc, obj)) break;
-    D = normalize(reflect(D, N), zero_events);
+    int ze = 0;
+    D = normalize(reflect(D, N), ze);
+    if (lvl == 1) zp += ze;
+    else zero_events += ze;
     float t;
     const int i = nearest(sc, O, D, S, t);
     if (i >= 0) {
@@ -498,6 +509,8 @@ __device__ __forceinline__ void shoot(const Scene& sc, V3 d, int maxrec, V3 carr
         const V3 A = normalize_sel(reflect(D, N));
         const V3 B = normalize_sel(reflect(A, N));
         po.dep = DepRec{A.x, A.y, A.z, N.x, N.y, N.z, obj, 0, B.x, B.y, B.z, 0};
+        if (MODE == kModeParityA && sc.dep_fast) po.pcol = shade(sc, i0, P0, N0, d, zp);
+        zero_events += zp;
         return;
       }
     }
@@ -512,20 +525,55 @@ __device__ __forceinline__ void shoot(const Scene& sc, V3 d, int maxrec, V3 carr
     S = i;
   }
   if (MODE != kModeClassify) {
-    V3 col = shade(sc, i0, P0, N0, d, zero_events);    // C/raycast.c:377-378
+    V3 col = shade(sc, i0, P0, N0, d, zp);             // C/raycast.c:377-378
     out = v3(out.x + col.x, out.y + col.y, out.z + col.z);
   }
+  zero_events += zp;
   po.rgb = out;
   po.cls = wrote ? kClsWriter : kClsIdent;
   po.carry = C;
 }
 
+// Phase C of a DEP pixel under dep_fast, from its carry-in c: the bounce loop of
+// iterative_shoot (C/raycast.c:348-376) resumed at level 2, then the primary shade phase A
+// computed (pcol, C/raycast.c:377-378).  Level 1 missed: its shade is the black phantom's
+// (exactly zero), O = C = c, S = -1, N = N0, obj = obj0, T = refl[obj0]^2, and level 2's
+// direction normalize(reflect(D1, N0)) is the record's `a`.
+__device__ __forceinline__ V3 shade_dep_cont(const Scene& sc, const DepRec& r, int maxrec, V3 c,
+                                             V3 pcol, int& zero_events) {
+  int obj = r.obj0, S = -1;
+  const float T0 = sc.lshapes[obj].refl;
+  float T = T0 * sc.lshapes[obj].refl;
+  V3 O = c, C = c, D = v3(r.ax, r.ay, r.az), N = v3(r.n0x, r.n0y, r.n0z);
+  V3 out = v3(0.0f, 0.0f, 0.0f);
+  for (int lvl = 2; lvl < maxrec; ++lvl) {
+    if (!reflective(sc, obj)) break;
+    if (lvl > 2) D = normalize(reflect(D, N), zero_events);
+    float t;
+    const int i = nearest(sc, O, D, S, t);
+    if (i >= 0) {
+      hit_frame(sc, i, O, D, t, C, N, zero_events);
+      obj = i;
+    }
+    const V3 col = shade(sc, i >= 0 ? i : sc.n, C, N, D, zero_events);
+    out.x = out.x + col.x * T;
+    out.y = out.y + col.y * T;
+    out.z = out.z + col.z * T;
+    T = T * sc.lshapes[obj].refl;
+    O = C;
+    S = i;
+  }
+  return v3(out.x + pcol.x, out.y + pcol.y, out.z + pcol.z);
+}
+
 // Carry-only continuation of a DEP pixel from carry-in c (levels 2..maxrec-1): the
 // phase-B transfer function f_p(c).  No shading: only the bounce-hit points matter.
+// `hit`: some level hit (the entry is not clean, see Scene::dep_fast).
 __device__ __forceinline__ V3 carry_path(const Scene& sc, const DepRec& r, int maxrec, V3 c,
-                                         int& zero_events) {
+                                         int& zero_events, bool& hit) {
   V3 D = v3(r.ax, r.ay, r.az), N = v3(r.n0x, r.n0y, r.n0z), C = c;   // level 2's direction
   int obj = r.obj0, S = -1;
+  hit = false;
   for (int lvl = 2; lvl < maxrec; ++lvl) {
     if (!reflective(sc, obj)) break;
     if (lvl > 2) D = normalize(reflect(D, N), zero_events);
@@ -536,6 +584,7 @@ __device__ __forceinline__ V3 carry_path(const Scene& sc, const DepRec& r, int m
       hit_frame(sc, i, C, D, t, P, N, zero_events);
       C = P;
       obj = i;
+      hit = true;
     }
     S = i;
   }
@@ -623,10 +672,11 @@ __device__ __forceinline__ int group_argmin_pos(float& t, int k, int G) {
 
 __device__ __forceinline__ V3 carry_path_coop(const Scene& sc, const LaneShape& ls, int kself,
                                               int G, const DepRec& r, int maxrec, V3 c,
-                                              int& zero_events) {
+                                              int& zero_events, bool& anyhit) {
   constexpr int kNone = 0x7fffffff;
   V3 D = v3(r.ax, r.ay, r.az), N = v3(r.n0x, r.n0y, r.n0z), C = c;   // level 2's direction
   int obj = r.obj0, S = -1;
+  anyhit = false;
   for (int lvl = 2; lvl < maxrec; ++lvl) {
     if (!reflective(sc, obj)) break;
     if (lvl > 2) D = normalize(reflect(D, N), zero_events);
@@ -647,6 +697,7 @@ __device__ __forceinline__ V3 carry_path_coop(const Scene& sc, const LaneShape& 
       C = P;
       obj = win;
       S = win;
+      anyhit = true;
     } else {
       S = -1;
     }
@@ -819,12 +870,13 @@ __device__ __forceinline__ void hit_frame_sel(const rc_shape& s, V3 O, V3 D, flo
 template <int GT, bool kQuad>
 __device__ __forceinline__ V3 carry_path_spec(const Scene& sc, const LaneShape& ls, int kself,
                                               int Grt, int half, const DepRec& r, int maxrec,
-                                              V3 c, int& zero_events
+                                              V3 c, int& zero_events, bool& anyhit
 #if RC_STAMPS
                                               , Stamps* st_
 #endif
 ) {
   (void)zero_events;
+  anyhit = false;
   const int G = GT ? GT : Grt;
   constexpr int kNone = 0x7fffffff;
   V3 N = v3(r.n0x, r.n0y, r.n0z), C = c;
@@ -871,6 +923,7 @@ __device__ __forceinline__ V3 carry_path_spec(const Scene& sc, const LaneShape& 
     const float tw = hitL ? t0 : t1;
     const V3 Dw = sel(two, D2, D1);
     const bool hit = w != kNone;
+    anyhit = anyhit | hit;
     V3 P, Nw;
     hit_frame_sel<kQuad>(sc.shapes[hit ? w : 0], C, Dw, tw, P, Nw);
     C = sel(hit, P, C);

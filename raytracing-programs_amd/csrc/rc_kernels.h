@@ -18,6 +18,7 @@ struct LaunchScene {
   float cam_w, cam_h;
   unsigned long long refl_mask;   // bit k: shape k reflective (n <= 64)
   int has_quadric;                // the scene has a quadric
+  int dep_fast;                   // clean DEP entries take phase A's primary shade (Scene)
 };
 
 // Parity-mode workspace (device pointers), sized for W*H pixels.

@@ -129,7 +129,11 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_
   shoot<kModeParityA>(sc, d, maxrec, v3(0.0f, 0.0f, 0.0f), po, zero);
   cls[p] = po.cls;
   if (po.cls == kClsDep) {
-    deprec[p] = po.dep;     // phase C recomputes the whole pixel (and counts its events)
+    deprec[p] = po.dep;
+    if (sc.dep_fast) {      // primary shade for phase C; this part's events are counted here
+      wcarry[p] = make_float4(po.pcol.x, po.pcol.y, po.pcol.z, 0.0f);
+      flush_events(zero, zcount);
+    }                       // else phase C recomputes the whole pixel (and counts its events)
     return;
   }
   if (po.cls == kClsWriter) wcarry[p] = make_float4(po.carry.x, po.carry.y, po.carry.z, 0.0f);
@@ -420,7 +424,8 @@ struct WinStats {
 __device__ __forceinline__ int wave_window(const Scene& sc, int maxrec,
                                            const DepRec* __restrict__ deprec,
                                            const long long* __restrict__ dep_pix, int base,
-                                           int end, V3& c, V3& mine, const LaneShape& ls,
+                                           int end, V3& c, V3& mine, bool& mhit,
+                                           const LaneShape& ls,
                                            int G, bool& dense, bool& changed,
                                            WinStats& ws, int K
 #if RC_STAMPS
@@ -434,6 +439,7 @@ __device__ __forceinline__ int wave_window(const Scene& sc, int maxrec,
   DepRec r;
   if (valid) r = rec_at(deprec, dep_pix, idx);
   mine = c;
+  mhit = false;
   changed = false;
   int zero = 0;
   int evals = 0;
@@ -450,15 +456,22 @@ __device__ __forceinline__ int wave_window(const Scene& sc, int maxrec,
       ++ws.lane;
       const bool act = valid && lane >= pos;
       V3 o = c;
-      if (act) o = carry_path(sc, r, maxrec, c, zero);
+      bool h = false;
+      if (act) o = carry_path(sc, r, maxrec, c, zero, h);
       const unsigned long long m = __ballot(act && !same_bits(o, c));
       if (m == 0) {
-        if (act) mine = c;
+        if (act) {
+          mine = c;
+          mhit = h;
+        }
         pos = nvalid;
         break;
       }
       const int k = __ffsll((long long)m) - 1;
-      if (act && lane <= k) mine = c;
+      if (act && lane <= k) {
+        mine = c;
+        mhit = h;
+      }
       c = v3(__shfl(o.x, k, 64), __shfl(o.y, k, 64), __shfl(o.z, k, 64));
       pos = k + 1;
       changed = true;
@@ -472,10 +485,11 @@ __device__ __forceinline__ int wave_window(const Scene& sc, int maxrec,
     const bool act = e < E && i < nvalid;
     const DepRec ri = shfl_rec(r, i < 64 ? i : 63);
     V3 oc = c;
+    bool hg = false;
 #if RC_STAMPS
-#define RC_SPEC1(GT, Q) carry_path_spec<GT, Q>(sc, ls, kself, G, half, ri, maxrec, c, zero, st_)
+#define RC_SPEC1(GT, Q) carry_path_spec<GT, Q>(sc, ls, kself, G, half, ri, maxrec, c, zero, hg, st_)
 #else
-#define RC_SPEC1(GT, Q) carry_path_spec<GT, Q>(sc, ls, kself, G, half, ri, maxrec, c, zero)
+#define RC_SPEC1(GT, Q) carry_path_spec<GT, Q>(sc, ls, kself, G, half, ri, maxrec, c, zero, hg)
 #endif
 #define RC_SPEC(GT) (sc.has_quadric ? RC_SPEC1(GT, true) : RC_SPEC1(GT, false))
     if (act) {
@@ -483,20 +497,29 @@ __device__ __forceinline__ int wave_window(const Scene& sc, int maxrec,
       else if (G == 4) oc = RC_SPEC(4);
       else if (G == 16) oc = RC_SPEC(16);
       else if (spec) oc = RC_SPEC(0);
-      else oc = carry_path_coop(sc, ls, kself, G, ri, maxrec, c, zero);
+      else oc = carry_path_coop(sc, ls, kself, G, ri, maxrec, c, zero, hg);
     }
 #undef RC_SPEC
 #undef RC_SPEC1
     const unsigned long long mc = __ballot(act && (lane % GE) == 0 && !same_bits(oc, c));
+    // entry pos+q's hit flag sits in its group's first lane, q*GE
+    const int q = lane - pos;
+    const bool hq = __shfl((int)hg, (q >= 0 && q < E ? q : 0) * GE, 64) != 0;
     if (mc == 0) {
       const int lim = pos + E < nvalid ? pos + E : nvalid;
-      if (lane >= pos && lane < lim) mine = c;
+      if (lane >= pos && lane < lim) {
+        mine = c;
+        mhit = hq;
+      }
       pos = lim;
       if (++clean_run >= K) coop = false;
       continue;
     }
     const int g = (__ffsll((long long)mc) - 1) / GE;
-    if (lane >= pos && lane <= pos + g) mine = c;
+    if (lane >= pos && lane <= pos + g) {
+      mine = c;
+      mhit = hq;
+    }
     c = v3(__shfl(oc.x, g * GE, 64), __shfl(oc.y, g * GE, 64), __shfl(oc.z, g * GE, 64));
     pos += g + 1;
     changed = true;
@@ -519,15 +542,19 @@ __device__ __forceinline__ unsigned long long pack2(unsigned lo, unsigned hi) {
 struct CinG {
   unsigned long long g[3];
 };
-__device__ __forceinline__ void cin_put(CinG* cin, int j, V3 c, unsigned tag) {
-  __hip_atomic_store(&cin[j].g[0], pack2(__float_as_uint(c.x), tag), __ATOMIC_RELAXED,
+// The tag's top bit carries the entry's hit flag (some bounce level hit at this carry-in:
+// not clean, Scene::dep_fast); epochs stay below 2^31.
+constexpr unsigned kCinHit = 0x80000000u;
+__device__ __forceinline__ void cin_put(CinG* cin, int j, V3 c, unsigned tag, bool hit) {
+  const unsigned tg = tag | (hit ? kCinHit : 0u);
+  __hip_atomic_store(&cin[j].g[0], pack2(__float_as_uint(c.x), tg), __ATOMIC_RELAXED,
                      __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store(&cin[j].g[1], pack2(__float_as_uint(c.y), tag), __ATOMIC_RELAXED,
+  __hip_atomic_store(&cin[j].g[1], pack2(__float_as_uint(c.y), tg), __ATOMIC_RELAXED,
                      __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store(&cin[j].g[2], pack2(__float_as_uint(c.z), tag), __ATOMIC_RELAXED,
+  __hip_atomic_store(&cin[j].g[2], pack2(__float_as_uint(c.z), tg), __ATOMIC_RELAXED,
                      __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ bool cin_get(CinG* cin, int j, unsigned tag, V3& c) {
+__device__ __forceinline__ bool cin_get(CinG* cin, int j, unsigned tag, V3& c, bool& hit) {
   const unsigned long long a =
       __hip_atomic_load(&cin[j].g[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const unsigned long long b =
@@ -536,8 +563,9 @@ __device__ __forceinline__ bool cin_get(CinG* cin, int j, unsigned tag, V3& c) {
       __hip_atomic_load(&cin[j].g[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   c = v3(__uint_as_float((unsigned)a), __uint_as_float((unsigned)b),
          __uint_as_float((unsigned)d));
-  return (unsigned)(a >> 32) == tag && (unsigned)(b >> 32) == tag &&
-         (unsigned)(d >> 32) == tag;
+  const unsigned ta = (unsigned)(a >> 32);
+  hit = (ta & kCinHit) != 0u;
+  return (ta & ~kCinHit) == tag && (unsigned)(b >> 32) == ta && (unsigned)(d >> 32) == ta;
 }
 
 // Resolver queue order: segments longest first (LPT), so the chains that take longest start
@@ -591,6 +619,7 @@ __global__ void __launch_bounds__(1024) k_seg_order(const int* __restrict__ seg_
 // resolve.  Every thread of the block must call this.
 struct BlockWinShared {
   DepRec rec[kResolveBlock];
+  uint8_t hit[kResolveBlock];   // per entry: some level hit at the window's carry
   int wpos[2][4];
   float wout[2][4][3];
 };
@@ -621,7 +650,9 @@ __device__ __forceinline__ void block_window(const Scene& sc, int maxrec, BlockW
       ++ws.lane;
       const bool act = t >= pos && t < nvalid;
       V3 o = c;
-      if (act) o = carry_path(sc, bw.rec[t], maxrec, c, zero);
+      bool h = false;
+      if (act) o = carry_path(sc, bw.rec[t], maxrec, c, zero, h);
+      bw.hit[t] = h ? 1 : 0;
       const unsigned long long m = __ballot(act && !same_bits(o, c));
       const int k = m ? __ffsll((long long)m) - 1 : -1;
       if (lane == 0) bw.wpos[par][wave] = k >= 0 ? wave * 64 + k : kNo;
@@ -636,11 +667,12 @@ __device__ __forceinline__ void block_window(const Scene& sc, int maxrec, BlockW
       const bool act = e < E && i < nvalid;
       const DepRec ri = bw.rec[i < nvalid ? i : pos];
       V3 oc = c;
+      bool hg = false;
 #if RC_STAMPS
       Stamps stq = {{0, 0, 0, 0}, 0};
-#define RC_SPEC1(GT, Q) carry_path_spec<GT, Q>(sc, ls, kself, G, half, ri, maxrec, c, zero, &stq)
+#define RC_SPEC1(GT, Q) carry_path_spec<GT, Q>(sc, ls, kself, G, half, ri, maxrec, c, zero, hg, &stq)
 #else
-#define RC_SPEC1(GT, Q) carry_path_spec<GT, Q>(sc, ls, kself, G, half, ri, maxrec, c, zero)
+#define RC_SPEC1(GT, Q) carry_path_spec<GT, Q>(sc, ls, kself, G, half, ri, maxrec, c, zero, hg)
 #endif
 #define RC_SPEC(GT) (sc.has_quadric ? RC_SPEC1(GT, true) : RC_SPEC1(GT, false))
       if (act) {
@@ -648,10 +680,11 @@ __device__ __forceinline__ void block_window(const Scene& sc, int maxrec, BlockW
         else if (G == 4) oc = RC_SPEC(4);
         else if (G == 16) oc = RC_SPEC(16);
         else if (spec) oc = RC_SPEC(0);
-        else oc = carry_path_coop(sc, ls, kself, G, ri, maxrec, c, zero);
+        else oc = carry_path_coop(sc, ls, kself, G, ri, maxrec, c, zero, hg);
       }
 #undef RC_SPEC
 #undef RC_SPEC1
+      if (act && (lane % GE) == 0) bw.hit[i] = hg ? 1 : 0;
       const unsigned long long mc = __ballot(act && (lane % GE) == 0 && !same_bits(oc, c));
       const int g = mc ? (__ffsll((long long)mc) - 1) / GE : -1;
       if (lane == 0) bw.wpos[par][wave] = g >= 0 ? pos + wave * E + g : kNo;
@@ -678,7 +711,7 @@ __device__ __forceinline__ void block_window(const Scene& sc, int maxrec, BlockW
     } else {
       last = coop ? (pos + Eb < nvalid ? pos + Eb : nvalid) - 1 : nvalid - 1;
     }
-    if (t >= pos && t <= last) cin_put(cin, base + t, c, tag);
+    if (t >= pos && t <= last) cin_put(cin, base + t, c, tag, bw.hit[t] != 0);
     pos = last + 1;
     c = cn;
     par ^= 1;
@@ -829,9 +862,10 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
           const int idx = base + lane;
           const bool valid = idx < end;
           V3 o = c;
+          bool h = false;
           if (valid) {
             int zero = 0;
-            o = carry_path(sc, rec_at(deprec, dep_pix, idx), maxrec, c, zero);
+            o = carry_path(sc, rec_at(deprec, dep_pix, idx), maxrec, c, zero, h);
           }
           const unsigned long long m = __ballot(valid && !same_bits(o, c));
           const int k = m ? __ffsll((long long)m) - 1 : -1;
@@ -874,7 +908,7 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
           __syncthreads();
           const int gpos = s_gpos;
           // entries before the first changer, and the changer itself, read carry c
-          if (valid && idx <= gpos) cin_put(cin, idx, c, tag);
+          if (valid && idx <= gpos) cin_put(cin, idx, c, tag, h);
           if (gpos == 0x7fffffff) {
             j += window;
           } else {
@@ -964,14 +998,15 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
     WinStats ws = {0, 0, 0};
     for (int j = start; j < end; j += 64) {
       V3 mine;
-      bool changed;
-      iters += wave_window(sc, maxrec, deprec, dep_pix, j, end, c, mine, ls, G, dense, changed, ws,
+      bool mhit, changed;
+      iters += wave_window(sc, maxrec, deprec, dep_pix, j, end, c, mine, mhit, ls, G, dense,
+                           changed, ws,
                            wave_k
 #if RC_STAMPS
                            , &stp
 #endif
                            );
-      if (j + lane < end) cin_put(cin, j + lane, mine, tag);
+      if (j + lane < end) cin_put(cin, j + lane, mine, tag, mhit);
     }
 #if RC_STAMPS
     if (trace && lane == 0 && end - start > 1000) {
@@ -1010,12 +1045,12 @@ __device__ __forceinline__ bool batch_claim(int* state, int b) {
 
 // Loads batch b's carry-ins; false if `wait` is false and one is not published yet.
 __device__ __forceinline__ bool batch_carries(CinG* cin, int ndep, int b, unsigned tag,
-                                              bool wait, V3& c, TeamState* ts) {
+                                              bool wait, V3& c, bool& hit, TeamState* ts) {
   const int j = b * 64 + (int)(threadIdx.x & 63);
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   for (;;) {
     bool ok = true;
-    if (j < ndep) ok = cin_get(cin, j, tag, c);
+    if (j < ndep) ok = cin_get(cin, j, tag, c, hit);
     if (__all(ok)) return true;
     if (!wait) return false;
     if (__builtin_amdgcn_s_memrealtime() - t0 > 500000000ull) {   // 5 s
@@ -1027,13 +1062,25 @@ __device__ __forceinline__ bool batch_carries(CinG* cin, int ndep, int b, unsign
   }
 }
 
+// Phase C of one batch of 64 DEP entries.  Under dep_fast phase A left each entry's primary
+// shade in wcarry[p] and counted the events of its primary part: a clean entry (no level hit
+// at its carry-in) is exactly that shade (every level's shade is zero, C/raycast.c:366-378),
+// the others resume at level 2 (shade_dep_cont).  Otherwise the pixel is recomputed.
 __device__ __forceinline__ void shade_batch(const Scene& sc, const Cam& cam, int W, int maxrec,
-                                            const long long* __restrict__ dep_pix, int ndep,
-                                            int b, V3 c, uint8_t* __restrict__ out,
+                                            const long long* __restrict__ dep_pix,
+                                            const DepRec* __restrict__ deprec,
+                                            const float4* __restrict__ pcol, int ndep, int b,
+                                            V3 c, bool hit, uint8_t* __restrict__ out,
                                             int& zero) {
   const int j = b * 64 + (int)(threadIdx.x & 63);
   if (j >= ndep) return;
   const long long p = dep_pix[j];
+  if (sc.dep_fast) {
+    const float4 k = pcol[p];
+    const V3 pc = v3(k.x, k.y, k.z);
+    store_rgb(out + (size_t)p * 3, hit ? shade_dep_cont(sc, deprec[p], maxrec, c, pc, zero) : pc);
+    return;
+  }
   const int y = (int)(p / W), x = (int)(p % W);
   const V3 d = primary_dir(cam, x, y, zero);
   PixelOut po;
@@ -1066,6 +1113,8 @@ __device__ __forceinline__ void shade_tile(const Scene& sc, const Cam& cam, int 
 // Phase C pass 1 (published batches) and pass 2 (everything unclaimed, waiting).
 __device__ __forceinline__ void phase_c_passes(const Scene& sc, const Cam& cam, int W,
                                                int maxrec, const long long* __restrict__ dep_pix,
+                                               const DepRec* __restrict__ deprec,
+                                               const float4* __restrict__ pcol,
                                                CinG* __restrict__ cin, int* __restrict__ counters,
                                                int* __restrict__ batch_state,
                                                uint8_t* __restrict__ out, TeamState* ts,
@@ -1077,11 +1126,12 @@ __device__ __forceinline__ void phase_c_passes(const Scene& sc, const Cam& cam, 
     const int b = wave_ticket(&counters[4]);
     if (b >= nb) break;
     V3 c = v3(0.0f, 0.0f, 0.0f);
-    if (!batch_carries(cin, ndep, b, tag, false, c, ts)) continue;
+    bool hit = true;
+    if (!batch_carries(cin, ndep, b, tag, false, c, hit, ts)) continue;
     int mine = 0;
     if ((threadIdx.x & 63) == 0) mine = batch_claim(batch_state, b);
     if (!__shfl(mine, 0, 64)) continue;
-    shade_batch(sc, cam, W, maxrec, dep_pix, ndep, b, c, out, zero);
+    shade_batch(sc, cam, W, maxrec, dep_pix, deprec, pcol, ndep, b, c, hit, out, zero);
     if ((threadIdx.x & 63) == 0) atomicAdd(done_ctr, 1);
   }
   for (;;) {
@@ -1091,8 +1141,9 @@ __device__ __forceinline__ void phase_c_passes(const Scene& sc, const Cam& cam, 
     if ((threadIdx.x & 63) == 0) mine = batch_claim(batch_state, b);
     if (!__shfl(mine, 0, 64)) continue;
     V3 c = v3(0.0f, 0.0f, 0.0f);
-    (void)batch_carries(cin, ndep, b, tag, true, c, ts);
-    shade_batch(sc, cam, W, maxrec, dep_pix, ndep, b, c, out, zero);
+    bool hit = true;
+    (void)batch_carries(cin, ndep, b, tag, true, c, hit, ts);
+    shade_batch(sc, cam, W, maxrec, dep_pix, deprec, pcol, ndep, b, c, hit, out, zero);
     if ((threadIdx.x & 63) == 0) atomicAdd(done_ctr, 1);
   }
 }
@@ -1100,7 +1151,8 @@ __device__ __forceinline__ void phase_c_passes(const Scene& sc, const Cam& cam, 
 template <bool kStage>
 __global__ void __launch_bounds__(kSideBlock) k_side(
     Scene sc, Cam cam, int W, int H, int maxrec, const uint8_t* __restrict__ cls,
-    const long long* __restrict__ dep_pix, CinG* __restrict__ cin, int* __restrict__ counters,
+    const long long* __restrict__ dep_pix, const DepRec* __restrict__ deprec,
+    const float4* __restrict__ pcol, CinG* __restrict__ cin, int* __restrict__ counters,
     int* __restrict__ batch_state, uint8_t* __restrict__ out,
     unsigned long long* __restrict__ zcount, TeamState* __restrict__ ts, int resolve_blocks,
     unsigned tag, int tiles) {
@@ -1135,7 +1187,7 @@ __global__ void __launch_bounds__(kSideBlock) k_side(
     shade_tile(sc, cam, W, H, maxrec, t, cls, out, zero);
     if ((threadIdx.x & 63) == 0) atomicAdd(&counters[8], 1);
   }
-  phase_c_passes(sc, cam, W, maxrec, dep_pix, cin, counters, batch_state, out, ts, tag, true,
+  phase_c_passes(sc, cam, W, maxrec, dep_pix, deprec, pcol, cin, counters, batch_state, out, ts, tag, true,
                  zero);
   flush_events(zero, zcount);
 }
@@ -1144,7 +1196,8 @@ __global__ void __launch_bounds__(kSideBlock) k_side(
 template <bool kStage>
 __global__ void __launch_bounds__(kBlock) k_finish(
     Scene sc, Cam cam, int W, int H, int maxrec, const uint8_t* __restrict__ cls,
-    const long long* __restrict__ dep_pix, CinG* __restrict__ cin, int* __restrict__ counters,
+    const long long* __restrict__ dep_pix, const DepRec* __restrict__ deprec,
+    const float4* __restrict__ pcol, CinG* __restrict__ cin, int* __restrict__ counters,
     int* __restrict__ batch_state, uint8_t* __restrict__ out,
     unsigned long long* __restrict__ zcount, TeamState* __restrict__ ts, unsigned tag,
     int tiles) {
@@ -1158,7 +1211,7 @@ __global__ void __launch_bounds__(kBlock) k_finish(
     shade_tile(sc, cam, W, H, maxrec, t, cls, out, zero);
     if ((threadIdx.x & 63) == 0) atomicAdd(&counters[10], 1);
   }
-  phase_c_passes(sc, cam, W, maxrec, dep_pix, cin, counters, batch_state, out, ts, tag, false,
+  phase_c_passes(sc, cam, W, maxrec, dep_pix, deprec, pcol, cin, counters, batch_state, out, ts, tag, false,
                  zero);
   flush_events(zero, zcount);
 }
@@ -1175,6 +1228,7 @@ static Scene make_scene(const LaunchScene& s) {
   sc.m = s.m;
   sc.refl_mask = s.refl_mask;
   sc.has_quadric = s.has_quadric;
+  sc.dep_fast = s.dep_fast;
   return sc;
 }
 static bool stage_fits(const LaunchScene& s) {
@@ -1252,14 +1306,18 @@ hipError_t launch_parity(const LaunchScene& s, int W, int H, int maxrec, uint8_t
   if (w.side) {   // colours and phase C beside the resolver
     (void)hipStreamWaitEvent(w.side, w.fork, 0);
     hipLaunchKernelGGL(st ? k_side<true> : k_side<false>, dim3(w.side_blocks), dim3(kSideBlock), w.side_lds, w.side, sc, cam,
-                       W, H, maxrec, w.cls, w.dep_pix, (CinG*)w.cin, w.counters, w.batch_state,
+                       W, H, maxrec, w.cls, w.dep_pix, (const DepRec*)w.deprec, w.wcarry,
+                       (CinG*)w.cin, w.counters,
+                       w.batch_state,
                        out, zcount, (TeamState*)w.team, w.resolve_blocks, w.epoch,
                        w.split_shade);
     (void)hipEventRecord(w.join, w.side);
   }
   if (ev) (void)hipEventRecord(ev[2], stream);
   hipLaunchKernelGGL(st ? k_finish<true> : k_finish<false>, dim3(w.phase_c_blocks), dim3(kBlock), 0, stream, sc, cam, W, H,
-                     maxrec, w.cls, w.dep_pix, (CinG*)w.cin, w.counters, w.batch_state, out,
+                     maxrec, w.cls, w.dep_pix, (const DepRec*)w.deprec, w.wcarry,
+                       (CinG*)w.cin, w.counters, w.batch_state,
+                     out,
                      zcount, (TeamState*)w.team, w.epoch, (w.side && w.split_shade) ? 1 : 0);
   if (w.side) (void)hipStreamWaitEvent(stream, w.join, 0);
   if (ev) (void)hipEventRecord(ev[3], stream);

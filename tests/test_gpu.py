@@ -57,12 +57,13 @@ def test_configs(key, scenes, table):
     assert p3_md5(img) == table[key]["md5"], key
 
 
-@pytest.mark.parametrize("knob", ["RC_NO_SIDE", "RC_SPLIT_SHADE", "RC_RESOLVE_SHARED"])
+@pytest.mark.parametrize("knob", ["RC_NO_SIDE", "RC_SPLIT_SHADE", "RC_RESOLVE_SHARED",
+                                  "RC_NO_DEP_FAST"])
 def test_parity_schedules(knob, scenes, table, monkeypatch):
     """The parity pipeline's alternative schedules give the same bytes: phase C after the
     resolver only (RC_NO_SIDE), colours shaded beside the resolver (RC_SPLIT_SHADE), and no
     one-workgroup-per-CU reservation (RC_RESOLVE_SHARED, which also disables the side
-    stream)."""
+    stream), and every first-bounce-miss pixel recomputed in phase C (RC_NO_DEP_FAST)."""
     monkeypatch.setenv(knob, "1")
     for key in ("quadric:4096x4096:d6:parity", "reflection:2048x2048:d4:parity",
                 "quadric:333x517:d6:parity"):
@@ -88,6 +89,39 @@ def test_many_shapes_vs_oracle(n_shapes, tmp_path):
                 continue
             np.testing.assert_array_equal(rc.render(s, 96, 72, depth=d, mode=mode), want,
                                           err_msg=f"{n_shapes} shapes {mode} d{d}")
+
+
+ZERO_EVENT_PLANES = [((0, 0, 1), 0.5, ""), ((0, 0.6, 0.8), 0.5, ""), ((0, 0.28, 0.96), 0.5, ""),
+                     ((0.6, 0, 0.8), 0.4, "sphere, radius: 1.0, diffuse_color: [1, 0, 0], "
+                      "specular_color: [1, 1, 1], position: [0, 3, -2], reflectivity: 0.5, "
+                      "refractivity: 0.0, ior: 1.0\n")]
+
+
+@pytest.mark.parametrize("case", range(len(ZERO_EVENT_PLANES)))
+@pytest.mark.parametrize("fast_dep", [True, False])
+def test_zero_normalize_events(case, fast_dep, tmp_path, monkeypatch):
+    """Zero-length normalize events (C/v3math.c:183-187; raycast() prints one stderr line per
+    event): a point light exactly on the hit point of the 1x1 image's ray.  The pixel is a
+    first-bounce miss; phase A counts its primary part and phase C the rest, with the clean-
+    entry path (Scene::dep_fast) on or off.  Counts and bytes against the CPU oracle."""
+    nrm, refl, extra = ZERO_EVENT_PLANES[case]
+    path = tmp_path / "z.scene"
+    path.write_text("camera, width: 2.0, height: 2.0\n"
+                    f"plane, normal: [{nrm[0]}, {nrm[1]}, {nrm[2]}], diffuse_color: [0.3, 0.5, 0.7], "
+                    f"specular_color: [1, 1, 1], position: [0, 0, -5], reflectivity: {refl}\n"
+                    + extra +
+                    "light, color: [4, 4, 4], radial-a2: 0.01, radial-a1: 0.0125, "
+                    "radial-a0: 0.0125, position: [0, 0, -5]\n")
+    if not fast_dep:
+        monkeypatch.setenv("RC_NO_DEP_FAST", "1")
+    s = rc.Scene.from_file(str(path))
+    for w, h in ((1, 1), (2, 1), (3, 1), (1, 3)):
+        want, st = oracle_render(s, w, h, 6, "parity")
+        tim = {}
+        got = rc.render(s, w, h, depth=6, mode="parity", timing=tim)
+        np.testing.assert_array_equal(got, want, err_msg=f"{w}x{h}")
+        assert tim["zero_normalize"] == st["zero_normalize"], (w, h, tim, st["zero_normalize"])
+    assert oracle_render(s, 1, 1, 6, "parity")[1]["zero_normalize"] > 0
 
 
 def test_c5_8192(scenes, table):
