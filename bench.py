@@ -2,12 +2,17 @@
 """Benchmark: primary rays/s (= pixels/s) rendering quadric.scene at 4096x4096, bounce depth 6
 (MAX_RECURSION 7, C/raycast.c:14) — BASELINE.json's metric.
 
-A "step" is one full render of the image through the C-ABI (rc_render_device): scene already
-resident in HBM, output written to a device buffer, every kernel of the mode inside the
-timed region.  Parity mode (default, byte-identical to the reference): phase A + scan-order
-compaction + carry-chain resolver + phase C.  Fast mode: one render kernel.
+A "step" is one full render of the image through the C-ABI: scene already resident in HBM,
+every frame written to its own device buffer, every kernel of the mode inside the timed
+region.  Parity mode (default, byte-identical to the reference): phase A + scan-order
+compaction + carry-chain resolver + phase C, with two frames in flight (rc_frame_submit:
+the carry resolvers of consecutive frames run side by side on one CU partition while the
+pixel phases run on the other; DESIGN.md §frames in flight) — `value` is K frames' pixels
+over the time to finish all K.  `single_frame` reports one frame at a time
+(rc_render_device, the raycast() path; --inflight 1 makes that the measured step).
+Fast mode: one render kernel per frame.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--mode parity|fast]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--mode parity|fast] [--inflight 1|2]
 
 Multi-GPU (torchrun, one rank per GPU, RANK/LOCAL_RANK/WORLD_SIZE from the env):
   parity: the image's scan-order carry chain is one serial dependency,
@@ -117,13 +122,17 @@ def cpu_baseline(scene_path, size, depth):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--mode", default="parity", choices=["parity", "fast"])
     ap.add_argument("--size", type=int, default=4096)
     ap.add_argument("--depth", type=int, default=6)
     ap.add_argument("--scene", default="quadric")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--timed-only", action="store_true",
+                    help="launch nothing but the warmup and timed steps (no single-frame, "
+                         "end-to-end or CPU legs): the command profiled under rocprofv3, so its "
+                         "per-kernel averages are those of the timed launches")
     ap.add_argument("--inflight", type=int, default=2, choices=[1, 2],
                     help="parity frames in flight: 2 = rc_frame_submit (the next frame's pixel "
                          "phases beside this frame's resolver), 1 = one rc_render_device per step")
@@ -185,6 +194,24 @@ def main():
         torch.cuda.synchronize()
 
     pipe_tim = {}
+    single = None
+    if piped and not args.timed_only:
+        # latency and per-phase times of a lone frame (rc_render_device, the raycast() path),
+        # taken before the frame pipeline's CU-partitioned streams exist
+        for _ in range(2):
+            pkg.render_device(scene, W, H, out.data_ptr(), stream.cuda_stream,
+                              depth=args.depth, mode=mode)
+        torch.cuda.synchronize()
+        pkg.profile_begin()
+        ts = time.perf_counter()
+        for _ in range(5):
+            pkg.render_device(scene, W, H, out.data_ptr(), stream.cuda_stream,
+                              depth=args.depth, mode=mode)
+        torch.cuda.synchronize()
+        single_ms = (time.perf_counter() - ts) * 1e3 / 5
+        single_phases = pkg.profile_end()
+        single = {"ms": round(single_ms, 4), "value": round(W * H / (single_ms * 1e-3), 1),
+                  "note": "one frame at a time (rc_render_device); phases_ms are its phases"}
     for _ in range(args.warmup):
         step()
     drain()
@@ -202,33 +229,21 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     phases = pkg.profile_end()
-    single = None
-    if piped:
-        # per-phase times and latency of a lone frame (rc_render_device), for the record
-        for _ in range(2):
-            pkg.render_device(scene, W, H, out.data_ptr(), stream.cuda_stream,
-                              depth=args.depth, mode=mode)
-        torch.cuda.synchronize()
-        pkg.profile_begin()
-        ts = time.perf_counter()
-        for _ in range(5):
-            pkg.render_device(scene, W, H, out.data_ptr(), stream.cuda_stream,
-                              depth=args.depth, mode=mode)
-        torch.cuda.synchronize()
-        single_ms = (time.perf_counter() - ts) * 1e3 / 5
-        phases = pkg.profile_end()
-        single = {"ms": round(single_ms, 4), "value": round(W * H / (single_ms * 1e-3), 1),
-                  "resolve_ms_in_flight": round(pipe_tim.get("resolve_ms", 0.0), 4),
-                  "note": "one frame at a time (rc_render_device), phases_ms are its phases"}
+    if single:
+        phases = single_phases
+        single["resolve_ms_in_flight"] = round(pipe_tim.get("resolve_ms", 0.0), 4)
     tmax = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
     if world > 1:
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
     tmax = float(tmax.item())
 
     tim = {}
-    pkg.render_device(scene, W, H, (send if sharded else out).data_ptr(), stream.cuda_stream,
-                      depth=args.depth, mode=mode, row0=row0, row_step=step_rows, nrows=nrows,
-                      timing=tim)
+    if piped:
+        tim = pipe_tim
+    elif not args.timed_only:
+        pkg.render_device(scene, W, H, (send if sharded else out).data_ptr(), stream.cuda_stream,
+                          depth=args.depth, mode=mode, row0=row0, row_step=step_rows,
+                          nrows=nrows, timing=tim)
     torch.cuda.synchronize()
     if rank == 0:
         images = 1 if sharded else world
@@ -239,7 +254,8 @@ def main():
             dom_name, dom_ms = "k_resolve", phases["resolve_ms"]
             if piped and pipe_tim.get("resolve_ms"):   # the launches of the timed region
                 dom_ms = pipe_tim["resolve_ms"]
-            dom_flop = work["dep_flop_per_entry"] * tim["dep_pixels"] if work else None
+            dom_flop = (work["dep_flop_per_entry"] * tim["dep_pixels"]
+                        if work and tim.get("dep_pixels") else None)
             render_ms = phases["phase_a_ms"] + phases["phase_c_ms"]
         else:
             dom_name, dom_ms = "k_render", phases["render_ms"]
@@ -294,9 +310,9 @@ def main():
         }
         if single:
             line["single_frame"] = single
-        if world == 1 and not sharded:
+        if world == 1 and not sharded and not args.timed_only:
             line["end_to_end"] = end_to_end(pkg, scene, W, H, args.depth, mode)
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and not args.timed_only:
             line["cpu_baseline"] = cpu_baseline(scene_path, args.size, args.depth)
         print(json.dumps(line), flush=True)
     if world > 1:

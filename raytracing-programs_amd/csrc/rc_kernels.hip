@@ -1193,8 +1193,11 @@ __global__ void __launch_bounds__(kSideBlock) k_side(
 }
 
 // After the resolver: the tiles (when `tiles`) and DEP batches k_side has not claimed.
+#ifndef RC_FINISH_WAVES
+#define RC_FINISH_WAVES 4   // phase C is throughput work: occupancy over a few spilled registers
+#endif
 template <bool kStage>
-__global__ void __launch_bounds__(kBlock) k_finish(
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_FINISH_WAVES))) k_finish(
     Scene sc, Cam cam, int W, int H, int maxrec, const uint8_t* __restrict__ cls,
     const long long* __restrict__ dep_pix, const DepRec* __restrict__ deprec,
     const float4* __restrict__ pcol, CinG* __restrict__ cin, int* __restrict__ counters,
