@@ -144,9 +144,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("RC_BENCH_BACKEND", "nccl") != "nccl":   # 1-GPU rehearsal: ranks share GPUs
+        local %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = os.environ.get("RC_BENCH_BACKEND", "nccl")   # gloo: 1-GPU rehearsal only
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     pkg = load_pkg()
     scene_path = os.path.join(ROOT, "tests", "golden", "scenes", args.scene + ".scene")
     scene = pkg.Scene.from_file(scene_path)

@@ -65,7 +65,7 @@ struct FrameBufs {
   DevBuf scene;         // uploaded packed scene
   const void* scene_src = nullptr;   // host image last uploaded
   DevBuf cls, wcarry, deprec, rows, dep_pix, seg_key, seg_start, seg_order, batch_state, cin,
-      counters, team, trace;
+      counters, team, trace, heavy;
 };
 
 // Pipelined parity frames (rc_frame_submit).  The device's CUs are split in two partitions
@@ -77,11 +77,12 @@ struct FrameBufs {
 // resolver is latency-bound (its carry chains), so overlapping kLanes of them multiplies the
 // frame rate until partition B's pixel work becomes the bound.
 struct Pipe {
-  static constexpr int kSlots = 4;   // frame workspaces (a frame re-uses slot k after k's end)
-  static constexpr int kLanes = 2;   // resolvers in flight
+  static constexpr int kSlots = 8;   // frame workspaces (a frame re-uses slot k after k's end)
+  static constexpr int kLanes = 4;   // resolvers in flight (at most)
   bool init = false;
   int res_cus = 0;                   // CUs in partition A
-  int lanes = kLanes;                // resolver streams in use (RC_PIPE_RESOLVERS)
+  int lanes = 2;                     // resolver streams in use (RC_PIPE_RESOLVERS)
+  int slots = 4;                     // workspaces / pixel streams in use (RC_PIPE_SLOTS)
   hipStream_t pix[kSlots] = {}, res[kLanes] = {};
   hipEvent_t ready[kSlots] = {}, done[kSlots] = {};
   static constexpr int kEv = 64;     // resolver timing events of the last kEv frames
@@ -92,6 +93,7 @@ struct Pipe {
   long long total = 0;               // parity frames ever (slot / stream rotation)
   long long last = -1;               // slot of the last parity frame
   bool used[kSlots] = {};
+  bool rt_on = true;                 // resolver timing events recorded (RC_PIPE_NO_RT: off)
 };
 
 struct DevCtx {
@@ -244,7 +246,8 @@ int ensure_parity(DevCtx& c, FrameBufs& b, int W, int H, rc::ParityWork& w, int 
       b.seg_start.ensure(P * sizeof(int)) ||
       b.seg_order.ensure((size_t)rc::kSegOrderMax * sizeof(int)) ||
       b.batch_state.ensure((P / 64 + 2) * sizeof(int)) ||
-      b.counters.ensure(64) || b.team.ensure(rc::team_state_bytes()))
+      b.counters.ensure(64) || b.team.ensure(rc::team_state_bytes()) ||
+      b.heavy.ensure(P * sizeof(int)))
     return -1;
   if (P >= (size_t)1 << 31) return -1;   // DEP indices are 32-bit
   // carry-ins are tagged with a per-frame epoch: a fresh buffer starts at tag 0, which no
@@ -331,6 +334,8 @@ int ensure_parity(DevCtx& c, FrameBufs& b, int W, int H, rc::ParityWork& w, int 
     w.trace = (unsigned*)b.trace.p;
   }
   w.phase_c_blocks = (piped ? c.cus - res_cus : c.cus) * 8;
+  w.heavy = (int*)b.heavy.p;
+  w.phase_c_finish = std::getenv("RC_PHASE_C_FINISH") ? 1 : 0;
   return 0;
 }
 
@@ -519,12 +524,12 @@ void pipe_release_all() {
     if (!p.init) continue;
     (void)hipSetDevice(c.device);
     (void)hipDeviceSynchronize();
-    for (int k = 0; k < Pipe::kSlots; ++k) {
+    for (int k = 0; k < p.slots; ++k) {
       (void)hipStreamDestroy(p.pix[k]);
       (void)hipEventDestroy(p.ready[k]);
       (void)hipEventDestroy(p.done[k]);
     }
-    for (int r = 0; r < Pipe::kLanes; ++r) (void)hipStreamDestroy(p.res[r]);
+    for (int r = 0; r < p.lanes; ++r) (void)hipStreamDestroy(p.res[r]);
     for (auto& e : p.rt) {
       (void)hipEventDestroy(e[0]);
       (void)hipEventDestroy(e[1]);
@@ -548,15 +553,19 @@ int pipe_init(DevCtx& c) {
   if (const char* e = std::getenv("RC_PIPE_RESOLVERS")) p.lanes = std::atoi(e);
   if (p.lanes < 1) p.lanes = 1;
   if (p.lanes > Pipe::kLanes) p.lanes = Pipe::kLanes;
+  if (const char* e = std::getenv("RC_PIPE_SLOTS")) p.slots = std::atoi(e);
+  if (p.slots < p.lanes + 1) p.slots = p.lanes + 1;
+  if (p.slots > Pipe::kSlots) p.slots = Pipe::kSlots;
+  p.rt_on = !std::getenv("RC_PIPE_NO_RT");
   res = res / (8 * p.lanes) * (8 * p.lanes);   // whole CUs per XCD for every resolver
   if (res < 16 * p.lanes) res = 16 * p.lanes;
   if (res > c.cus - 16) res = (c.cus - 16) / (8 * p.lanes) * (8 * p.lanes);
   const int words = (c.cus + 31) / 32;
   std::vector<uint32_t> ma(words, 0), mb(words, 0);
   for (int i = 0; i < c.cus; ++i) (i < res ? ma : mb)[i / 32] |= 1u << (i % 32);
-  for (int r = 0; r < Pipe::kLanes; ++r)
+  for (int r = 0; r < p.lanes; ++r)
     HIP_TRY(hipExtStreamCreateWithCUMask(&p.res[r], (uint32_t)words, ma.data()));
-  for (int k = 0; k < Pipe::kSlots; ++k) {
+  for (int k = 0; k < p.slots; ++k) {
     HIP_TRY(hipExtStreamCreateWithCUMask(&p.pix[k], (uint32_t)words, mb.data()));
     HIP_TRY(hipEventCreateWithFlags(&p.ready[k], hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&p.done[k], hipEventDisableTiming));
@@ -588,7 +597,7 @@ int rc_frame_submit(const rc_scene* s, int W, int H, const rc_options* opt, uint
   }
   if (pipe_init(*c)) return -1;
   Pipe& p = c->pipe;
-  const int k = (int)(p.total % Pipe::kSlots);
+  const int k = (int)(p.total % p.slots);
   const int lane = (int)(p.total % p.lanes);
   FrameBufs& b = p.fb[k];
   // A frame submitted into an empty pipeline has no resolver to hide behind: its phase A
@@ -610,8 +619,8 @@ int rc_frame_submit(const rc_scene* s, int W, int H, const rc_options* opt, uint
   w.rready = p.ready[k];
   w.rdone = p.done[k];
   const int e = (int)(p.submitted % Pipe::kEv);
-  w.rt0 = p.rt[e][0];
-  w.rt1 = p.rt[e][1];
+  w.rt0 = p.rt_on ? p.rt[e][0] : nullptr;
+  w.rt1 = p.rt_on ? p.rt[e][1] : nullptr;
   HIP_TRY(rc::launch_parity(ls, W, H, maxrec, d_out, w, zc, st, nullptr));
   p.submitted++;
   p.frames++;
@@ -631,9 +640,9 @@ int rc_frames_wait(rc_timing* timing) {
   HIP_TRY(hipStreamSynchronize(c->stream));
   int rc = 0;
   if (p.init) {
-    for (int k = 0; k < Pipe::kSlots; ++k) HIP_TRY(hipStreamSynchronize(p.pix[k]));
-    for (int r = 0; r < Pipe::kLanes; ++r) HIP_TRY(hipStreamSynchronize(p.res[r]));
-    for (int k = 0; k < Pipe::kSlots; ++k) {   // the last frame of each slot
+    for (int k = 0; k < p.slots; ++k) HIP_TRY(hipStreamSynchronize(p.pix[k]));
+    for (int r = 0; r < p.lanes; ++r) HIP_TRY(hipStreamSynchronize(p.res[r]));
+    for (int k = 0; k < p.slots; ++k) {   // the last frame of each slot
       if (!p.used[k] || !p.fb[k].team.p) continue;
       int err = 0;
       HIP_TRY(hipMemcpy(&err, p.fb[k].team.p, sizeof err, hipMemcpyDeviceToHost));
@@ -642,7 +651,7 @@ int rc_frames_wait(rc_timing* timing) {
         rc = -1;
       }
     }
-    const int n = p.submitted < Pipe::kEv ? (int)p.submitted : Pipe::kEv;
+    const int n = !p.rt_on ? 0 : p.submitted < Pipe::kEv ? (int)p.submitted : Pipe::kEv;
     double sum = 0.0;
     for (int e = 0; e < n; ++e) sum += event_ms(p.rt[e][0], p.rt[e][1]);
     if (n > 0) g_last_kernel_ms = sum / n;

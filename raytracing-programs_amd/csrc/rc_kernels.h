@@ -50,6 +50,8 @@ struct ParityWork {
   int team_blocks;          // workgroups in the long-segment team (0: no team)
   int long_len;             // segments with >= long_len entries go to the team
   int phase_c_blocks;       // grid-stride phase C grid
+  int* heavy;               // [P]   phase C after the resolver: non-clean DEP entries
+  int phase_c_finish;       // phase C after the resolver through k_finish's claims (RC_PHASE_C_FINISH)
   int wave_k;               // clean cooperative steps before a wave window goes back to LANE
   int resolve_k;            // the same for the team leader's block window
   int coop_group;           // lanes per entry of the cooperative evaluator (0: off)
@@ -60,6 +62,8 @@ struct ParityWork {
   hipStream_t pstream;      // phase C's stream (null: the main stream)
   hipEvent_t rready, rdone; // main -> rstream after compaction; rstream -> pstream after it
   hipEvent_t rt0, rt1;      // optional: resolver start / end on rstream
+  int defer_c;              // pipelined: launch_parity stops after the resolver; phase C is
+                            // enqueued later by launch_phase_c (after rdone)
 };
 
 constexpr int kSegOrderMax = 65536;   // segments ordered for the resolver queue (else FIFO)
@@ -73,6 +77,10 @@ hipError_t launch_render(const LaunchScene& s, int W, int H, int row0, int row_s
 hipError_t launch_parity(const LaunchScene& s, int W, int H, int maxrec, uint8_t* out,
                          const ParityWork& w, unsigned long long* zcount, hipStream_t stream,
                          const hipEvent_t* ev);
+
+// Phase C of a frame launched with defer_c: waits for w.rdone on `stream`.
+hipError_t launch_phase_c(const LaunchScene& s, int W, int H, int maxrec, uint8_t* out,
+                          const ParityWork& w, unsigned long long* zcount, hipStream_t stream);
 
 size_t deprec_bytes();
 size_t row_stats_bytes();

@@ -1219,6 +1219,85 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_
   flush_events(zero, zcount);
 }
 
+// Phase C after the resolver has finished (stream order: every carry-in is published), in
+// two grid-stride passes without claims or tickets:
+//   k_dep_split  one lane per DEP entry: a clean entry (dep_fast, no level hit at its
+//                carry-in) is its primary shade, stored here; the others are appended to
+//                the heavy list (wave-aggregated, lane order kept) — counters[14] entries.
+//   k_dep_heavy  one lane per heavy entry: levels 2.. with shading (shade_dep_cont), or the
+//                whole pixel again when the scene is not dep_fast.
+// Entries are independent once their carry-ins are known, so the list order is free; the
+// point is full waves of heavy work (~35 % of the entries are clean at quadric 4096^2).
+constexpr int kHeavyCounter = 14;
+
+__global__ void __launch_bounds__(256) k_dep_split(Scene sc, const long long* __restrict__ dep_pix,
+                                                  const float4* __restrict__ pcol,
+                                                  CinG* __restrict__ cin,
+                                                  int* __restrict__ counters,
+                                                  int* __restrict__ heavy,
+                                                  uint8_t* __restrict__ out,
+                                                  TeamState* __restrict__ ts, unsigned tag) {
+  const int ndep = counters[2];
+  const int nb = (ndep + 63) / 64;
+  const int lane = threadIdx.x & 63;
+  const int nw = (int)((gridDim.x * blockDim.x) >> 6);
+  for (int b = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6); b < nb; b += nw) {
+    const int j = b * 64 + lane;
+    V3 c = v3(0.0f, 0.0f, 0.0f);
+    bool hit = true;
+    (void)batch_carries(cin, ndep, b, tag, true, c, hit, ts);
+    const bool in = j < ndep;
+    const bool hv = in && (!sc.dep_fast || hit);
+    if (in && !hv) {
+      const long long p = dep_pix[j];
+      const float4 k = pcol[p];
+      store_rgb(out + (size_t)p * 3, v3(k.x, k.y, k.z));
+    }
+    const unsigned long long m = __ballot(hv);
+    int base = 0;
+    if (lane == 0 && m) base = atomicAdd(&counters[kHeavyCounter], __popcll(m));
+    base = __shfl(base, 0, 64);
+    if (hv) heavy[base + __popcll(m & lanemask_lt())] = j;
+  }
+}
+
+template <bool kStage>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_FINISH_WAVES))) k_dep_heavy(
+    Scene sc, Cam cam, int W, int maxrec, const long long* __restrict__ dep_pix,
+    const DepRec* __restrict__ deprec, const float4* __restrict__ pcol, CinG* __restrict__ cin,
+    const int* __restrict__ counters, const int* __restrict__ heavy,
+    uint8_t* __restrict__ out, unsigned long long* __restrict__ zcount, unsigned tag) {
+  __shared__ StageBuf<kStage> stage;
+  stage_scene<kStage>(sc, stage);
+  const int nh = counters[kHeavyCounter];
+  const int nb = (nh + 63) / 64;
+  const int lane = threadIdx.x & 63;
+  const int nw = (int)((gridDim.x * blockDim.x) >> 6);
+  int zero = 0;
+  for (int b = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6); b < nb; b += nw) {
+    const int k = b * 64 + lane;
+    if (k >= nh) continue;
+    const int j = heavy[k];
+    V3 c;
+    bool hit;
+    (void)cin_get(cin, j, tag, c, hit);   // published: k_dep_split checked every tag
+    const long long p = dep_pix[j];
+    V3 rgb;
+    if (sc.dep_fast) {
+      const float4 q = pcol[p];
+      rgb = shade_dep_cont(sc, deprec[p], maxrec, c, v3(q.x, q.y, q.z), zero);
+    } else {
+      const int y = (int)(p / W), x = (int)(p % W);
+      const V3 d = primary_dir(cam, x, y, zero);
+      PixelOut po;
+      shoot<kModeParityC>(sc, d, maxrec, c, po, zero);
+      rgb = po.rgb;
+    }
+    store_rgb(out + (size_t)p * 3, rgb);
+  }
+  flush_events(zero, zcount);
+}
+
 // ---------------------------------------------------------------------- launchers --
 static Scene make_scene(const LaunchScene& s) {
   Scene sc;
@@ -1254,6 +1333,10 @@ hipError_t launch_render(const LaunchScene& s, int W, int H, int row0, int row_s
                      W, H, row0, row_step, nrows, maxrec, out, zcount);
   return hipGetLastError();
 }
+
+static void enqueue_phase_c(const Scene& sc, const Cam& cam, bool st, int W, int H, int maxrec,
+                            uint8_t* out, const ParityWork& w, unsigned long long* zcount,
+                            hipStream_t stream);
 
 hipError_t launch_parity(const LaunchScene& s, int W, int H, int maxrec, uint8_t* out,
                          const ParityWork& w, unsigned long long* zcount, hipStream_t stream,
@@ -1303,6 +1386,7 @@ hipError_t launch_parity(const LaunchScene& s, int W, int H, int maxrec, uint8_t
   if (w.rstream) {
     if (w.rt1) (void)hipEventRecord(w.rt1, rs);
     (void)hipEventRecord(w.rdone, rs);
+    if (w.defer_c) return hipGetLastError();   // phase C: launch_phase_c, later
     if (w.pstream) stream = w.pstream;
     (void)hipStreamWaitEvent(stream, w.rdone, 0);
   }
@@ -1317,14 +1401,38 @@ hipError_t launch_parity(const LaunchScene& s, int W, int H, int maxrec, uint8_t
     (void)hipEventRecord(w.join, w.side);
   }
   if (ev) (void)hipEventRecord(ev[2], stream);
-  hipLaunchKernelGGL(st ? k_finish<true> : k_finish<false>, dim3(w.phase_c_blocks), dim3(kBlock), 0, stream, sc, cam, W, H,
-                     maxrec, w.cls, w.dep_pix, (const DepRec*)w.deprec, w.wcarry,
-                       (CinG*)w.cin, w.counters, w.batch_state,
-                     out,
-                     zcount, (TeamState*)w.team, w.epoch, (w.side && w.split_shade) ? 1 : 0);
+  enqueue_phase_c(sc, cam, st, W, H, maxrec, out, w, zcount, stream);
   if (w.side) (void)hipStreamWaitEvent(stream, w.join, 0);
   if (ev) (void)hipEventRecord(ev[3], stream);
   return hipGetLastError();
+}
+
+hipError_t launch_phase_c(const LaunchScene& s, int W, int H, int maxrec, uint8_t* out,
+                          const ParityWork& w, unsigned long long* zcount, hipStream_t stream) {
+  (void)hipStreamWaitEvent(stream, w.rdone, 0);
+  enqueue_phase_c(make_scene(s), make_cam(s, W, H), stage_fits(s), W, H, maxrec, out, w, zcount,
+                  stream);
+  return hipGetLastError();
+}
+
+static void enqueue_phase_c(const Scene& sc, const Cam& cam, bool st, int W, int H, int maxrec,
+                            uint8_t* out, const ParityWork& w, unsigned long long* zcount,
+                            hipStream_t stream) {
+  if (w.side || w.phase_c_finish) {   // what k_side has not claimed (or the claim-based form)
+    hipLaunchKernelGGL(st ? k_finish<true> : k_finish<false>, dim3(w.phase_c_blocks), dim3(kBlock), 0, stream, sc, cam, W, H,
+                       maxrec, w.cls, w.dep_pix, (const DepRec*)w.deprec, w.wcarry,
+                       (CinG*)w.cin, w.counters, w.batch_state,
+                       out,
+                       zcount, (TeamState*)w.team, w.epoch, (w.side && w.split_shade) ? 1 : 0);
+  } else {   // all of phase C after the resolver: clean entries, then full waves of the rest
+    hipLaunchKernelGGL(k_dep_split, dim3(w.phase_c_blocks), dim3(256), 0, stream, sc, w.dep_pix,
+                       (const float4*)w.wcarry, (CinG*)w.cin, w.counters, w.heavy, out,
+                       (TeamState*)w.team, w.epoch);
+    hipLaunchKernelGGL(st ? k_dep_heavy<true> : k_dep_heavy<false>, dim3(w.phase_c_blocks),
+                       dim3(kBlock), 0, stream, sc, cam, W, maxrec, w.dep_pix,
+                       (const DepRec*)w.deprec, (const float4*)w.wcarry, (CinG*)w.cin,
+                       w.counters, w.heavy, out, zcount, w.epoch);
+  }
 }
 
 size_t team_state_bytes() { return sizeof(TeamState); }

@@ -58,13 +58,17 @@ def test_configs(key, scenes, table):
 
 
 @pytest.mark.parametrize("knob", ["RC_NO_SIDE", "RC_SPLIT_SHADE", "RC_RESOLVE_SHARED",
-                                  "RC_NO_DEP_FAST"])
+                                  "RC_NO_DEP_FAST", "RC_NO_SIDE+RC_NO_DEP_FAST",
+                                  "RC_NO_SIDE+RC_PHASE_C_FINISH"])
 def test_parity_schedules(knob, scenes, table, monkeypatch):
     """The parity pipeline's alternative schedules give the same bytes: phase C after the
-    resolver only (RC_NO_SIDE), colours shaded beside the resolver (RC_SPLIT_SHADE), and no
-    one-workgroup-per-CU reservation (RC_RESOLVE_SHARED, which also disables the side
-    stream), and every first-bounce-miss pixel recomputed in phase C (RC_NO_DEP_FAST)."""
-    monkeypatch.setenv(knob, "1")
+    resolver only (RC_NO_SIDE: clean entries, then full waves of the rest — k_dep_split /
+    k_dep_heavy; with RC_PHASE_C_FINISH through k_finish's batch claims), colours shaded
+    beside the resolver (RC_SPLIT_SHADE), and no one-workgroup-per-CU reservation
+    (RC_RESOLVE_SHARED, which also disables the side stream), and every first-bounce-miss
+    pixel recomputed in phase C (RC_NO_DEP_FAST)."""
+    for k in knob.split("+"):
+        monkeypatch.setenv(k, "1")
     for key in ("quadric:4096x4096:d6:parity", "reflection:2048x2048:d4:parity",
                 "quadric:333x517:d6:parity"):
         scene, size, d, mode = key.split(":")
@@ -99,7 +103,8 @@ ZERO_EVENT_PLANES = [((0, 0, 1), 0.5, ""), ((0, 0.6, 0.8), 0.5, ""), ((0, 0.28, 
 
 @pytest.mark.parametrize("case", range(len(ZERO_EVENT_PLANES)))
 @pytest.mark.parametrize("fast_dep", [True, False])
-def test_zero_normalize_events(case, fast_dep, tmp_path, monkeypatch):
+@pytest.mark.parametrize("side", [True, False])
+def test_zero_normalize_events(case, fast_dep, side, tmp_path, monkeypatch):
     """Zero-length normalize events (C/v3math.c:183-187; raycast() prints one stderr line per
     event): a point light exactly on the hit point of the 1x1 image's ray.  The pixel is a
     first-bounce miss; phase A counts its primary part and phase C the rest, with the clean-
@@ -114,6 +119,8 @@ def test_zero_normalize_events(case, fast_dep, tmp_path, monkeypatch):
                     "radial-a0: 0.0125, position: [0, 0, -5]\n")
     if not fast_dep:
         monkeypatch.setenv("RC_NO_DEP_FAST", "1")
+    if not side:   # phase C after the resolver: k_dep_split / k_dep_heavy
+        monkeypatch.setenv("RC_NO_SIDE", "1")
     s = rc.Scene.from_file(str(path))
     for w, h in ((1, 1), (2, 1), (3, 1), (1, 3)):
         want, st = oracle_render(s, w, h, 6, "parity")
