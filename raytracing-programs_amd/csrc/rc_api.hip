@@ -115,6 +115,9 @@ struct DevCtx {
   Pipe pipe;
   int resident_blocks = 0;
   int resident_lds = -1;
+  static constexpr int kResCache = 4;   // resident resolver grids per LDS reservation
+  int res_lds[kResCache] = {};
+  int res_blocks[kResCache] = {};
   size_t parity_pixels = 0;
   int parity_rows = 0;
 };
@@ -260,12 +263,25 @@ int ensure_parity(DevCtx& c, FrameBufs& b, int W, int H, rc::ParityWork& w, int 
     if (hipMemset(b.cin.p, 0, b.cin.bytes) != hipSuccess) return -1;
     b.epoch = 1;
   }
+  const bool piped = res_cus != c.cus;
+  // Resolver placement by its dynamic LDS reservation: one workgroup (4 waves, one per SIMD)
+  // per CU for a lone frame, whose critical path is its carry chains (and k_side must stay off
+  // the resolver's CUs); two per CU for a pipeline lane, whose grid is small (64 CUs) — there
+  // the longest segments outnumber one-per-CU's waves and the chains that start late set the
+  // resolver's time (measured: 4.9e9 -> 5.4e9 rays/s with frames in flight, 6.37 -> 6.49 ms
+  // for a lone frame).
   const int one_per_cu = std::getenv("RC_RESOLVE_SHARED") ? 0 : 1;
-  const int lds = one_per_cu ? 96 * 1024 : 0;
-  if (!c.resident_blocks || c.resident_lds != lds) {
-    c.resident_blocks = rc::resolve_blocks_resident(c.cus, lds);
-    c.resident_lds = lds;
+  int lds = !one_per_cu ? 0 : piped ? 56 * 1024 : 96 * 1024;
+  if (const char* e = std::getenv("RC_RESOLVE_LDS_KB")) lds = std::atoi(e) * 1024;
+  int slot = 0;
+  while (slot < DevCtx::kResCache && c.res_lds[slot] != lds && c.res_blocks[slot]) ++slot;
+  if (slot == DevCtx::kResCache) slot = 0;
+  if (!c.res_blocks[slot] || c.res_lds[slot] != lds) {
+    c.res_blocks[slot] = rc::resolve_blocks_resident(c.cus, lds);
+    c.res_lds[slot] = lds;
   }
+  c.resident_blocks = c.res_blocks[slot];
+  c.resident_lds = lds;
   char* r = (char*)b.rows.p;
   w.cls = (uint8_t*)b.cls.p;
   w.wcarry = (float4*)b.wcarry.p;
@@ -281,7 +297,6 @@ int ensure_parity(DevCtx& c, FrameBufs& b, int W, int H, rc::ParityWork& w, int 
   w.seg_order = (int*)b.seg_order.p;
   w.cin = b.cin.p;
   w.batch_state = (int*)b.batch_state.p;
-  const bool piped = res_cus != c.cus;
   w.side = nullptr;
   w.rstream = nullptr;
   w.pstream = nullptr;
@@ -365,7 +380,10 @@ int enqueue_render(DevCtx& c, const rc_scene* s, int W, int H, int row0, int row
     return -1;
   }
   rc::ParityWork w{};
-  if (ensure_parity(c, c.fb, W, H, w, c.cus)) {
+  int res_cus = c.cus;   // diagnostic: RC_SINGLE_RES_CUS sizes the resolver like a pipeline lane's
+  if (const char* e = std::getenv("RC_SINGLE_RES_CUS")) res_cus = std::atoi(e);
+  if (res_cus < 8 || res_cus > c.cus) res_cus = c.cus;
+  if (ensure_parity(c, c.fb, W, H, w, res_cus)) {
     std::fprintf(stderr, "Error: out of device memory for the parity workspace\n");
     return -1;
   }

@@ -1473,11 +1473,16 @@ int phase_c_side_blocks(int cus, int side_lds) {
 }
 
 int resolve_blocks_resident(int cus, int lds_bytes) {
-  if (lds_bytes > 0) {
+  // the attribute is an upper bound for every launch: keep it at the largest reservation in
+  // use (lone frames 96 KiB, pipeline lanes 56 KiB)
+  static int max_set = 0;
+  const int cap = lds_bytes > 96 * 1024 ? lds_bytes : 96 * 1024;
+  if (cap > max_set) {
     (void)hipFuncSetAttribute((const void*)k_resolve<true>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
+                              hipFuncAttributeMaxDynamicSharedMemorySize, cap);
     (void)hipFuncSetAttribute((const void*)k_resolve<false>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes);
+                              hipFuncAttributeMaxDynamicSharedMemorySize, cap);
+    max_set = cap;
   }
   int per_cu = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_resolve<true>, kResolveBlock,

@@ -1,0 +1,35 @@
+"""Summarise an RC_RESOLVE_TRACE per-segment trace: when each segment starts/ends (10 ns
+ticks of s_memrealtime), which segments end last, team rounds.
+  python scripts/seg_trace.py TRACE"""
+import sys
+path = sys.argv[1]
+seg = {}
+for l in open(path):
+    if l.startswith("#"):
+        continue
+    k, start, ln, ticks, evals, cyc = map(int, l.split())
+    seg[k] = dict(start=start, len=ln, dur=ticks, evals=evals, cyc=cyc)
+for l in open(path + ".start"):
+    k, t = map(int, l.split())
+    if k in seg:
+        seg[k]["t0"] = t
+team = [k for k, d in seg.items() if d["evals"] & 0x80000000]
+t0s = [d["t0"] for k, d in seg.items() if k not in team and d.get("t0")]
+base = min(t0s) if t0s else 0
+ends = []
+for k, d in seg.items():
+    if k in team:
+        continue
+    t = (d.get("t0", base) - base) & 0xffffffff
+    ends.append(((t + d["dur"]) / 100.0, t / 100.0, d["dur"] / 100.0, d["len"], d["evals"], k))
+ends.sort(reverse=True)
+print("segments:", len(seg), "team:", len(team), "total entries:", sum(d["len"] for d in seg.values()))
+for k in team:
+    d = seg[k]
+    print(f"team seg {k}: len {d['len']} dur {d['dur']/100:.1f} us rounds {d['evals'] & 0x7fffffff}")
+print("last-ending regular segments (end_us start_us dur_us len evals seg):")
+for e in ends[:15]:
+    print("  %.1f %.1f %.1f %d %d %d" % e)
+busy = sum(d["dur"] for k, d in seg.items() if k not in team) / 100.0
+print(f"regular wave-time: {busy/1000:.1f} wave-ms; longest 10 durations (us):",
+      sorted((d["dur"] / 100 for k, d in seg.items() if k not in team), reverse=True)[:10])
