@@ -65,7 +65,7 @@ struct FrameBufs {
   DevBuf scene;         // uploaded packed scene
   const void* scene_src = nullptr;   // host image last uploaded
   DevBuf cls, wcarry, deprec, rows, dep_pix, seg_key, seg_start, seg_order, batch_state, cin,
-      counters, team, trace, heavy;
+      counters, team, trace;
 };
 
 // Pipelined parity frames (rc_frame_submit).  The device's CUs are split in two partitions
@@ -249,8 +249,7 @@ int ensure_parity(DevCtx& c, FrameBufs& b, int W, int H, rc::ParityWork& w, int 
       b.seg_start.ensure(P * sizeof(int)) ||
       b.seg_order.ensure((size_t)rc::kSegOrderMax * sizeof(int)) ||
       b.batch_state.ensure((P / 64 + 2) * sizeof(int)) ||
-      b.counters.ensure(64) || b.team.ensure(rc::team_state_bytes()) ||
-      b.heavy.ensure(P * sizeof(int)))
+      b.counters.ensure(64) || b.team.ensure(rc::team_state_bytes()))
     return -1;
   if (P >= (size_t)1 << 31) return -1;   // DEP indices are 32-bit
   // carry-ins are tagged with a per-frame epoch: a fresh buffer starts at tag 0, which no
@@ -349,7 +348,6 @@ int ensure_parity(DevCtx& c, FrameBufs& b, int W, int H, rc::ParityWork& w, int 
     w.trace = (unsigned*)b.trace.p;
   }
   w.phase_c_blocks = (piped ? c.cus - res_cus : c.cus) * 8;
-  w.heavy = (int*)b.heavy.p;
   w.phase_c_finish = std::getenv("RC_PHASE_C_FINISH") ? 1 : 0;
   return 0;
 }

@@ -50,7 +50,6 @@ struct ParityWork {
   int team_blocks;          // workgroups in the long-segment team (0: no team)
   int long_len;             // segments with >= long_len entries go to the team
   int phase_c_blocks;       // grid-stride phase C grid
-  int* heavy;               // [P]   phase C after the resolver: non-clean DEP entries
   int phase_c_finish;       // phase C after the resolver through k_finish's claims (RC_PHASE_C_FINISH)
   int wave_k;               // clean cooperative steps before a wave window goes back to LANE
   int resolve_k;            // the same for the team leader's block window

@@ -1219,81 +1219,80 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_
   flush_events(zero, zcount);
 }
 
-// Phase C after the resolver has finished (stream order: every carry-in is published), in
-// two grid-stride passes without claims or tickets:
-//   k_dep_split  one lane per DEP entry: a clean entry (dep_fast, no level hit at its
-//                carry-in) is its primary shade, stored here; the others are appended to
-//                the heavy list (wave-aggregated, lane order kept) — counters[14] entries.
-//   k_dep_heavy  one lane per heavy entry: levels 2.. with shading (shade_dep_cont), or the
-//                whole pixel again when the scene is not dep_fast.
-// Entries are independent once their carry-ins are known, so the list order is free; the
-// point is full waves of heavy work (~35 % of the entries are clean at quadric 4096^2).
-constexpr int kHeavyCounter = 14;
-
-__global__ void __launch_bounds__(256) k_dep_split(Scene sc, const long long* __restrict__ dep_pix,
-                                                  const float4* __restrict__ pcol,
-                                                  CinG* __restrict__ cin,
-                                                  int* __restrict__ counters,
-                                                  int* __restrict__ heavy,
-                                                  uint8_t* __restrict__ out,
-                                                  TeamState* __restrict__ ts, unsigned tag) {
-  const int ndep = counters[2];
-  const int nb = (ndep + 63) / 64;
-  const int lane = threadIdx.x & 63;
-  const int nw = (int)((gridDim.x * blockDim.x) >> 6);
-  for (int b = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6); b < nb; b += nw) {
-    const int j = b * 64 + lane;
-    V3 c = v3(0.0f, 0.0f, 0.0f);
-    bool hit = true;
-    (void)batch_carries(cin, ndep, b, tag, true, c, hit, ts);
-    const bool in = j < ndep;
-    const bool hv = in && (!sc.dep_fast || hit);
-    if (in && !hv) {
-      const long long p = dep_pix[j];
-      const float4 k = pcol[p];
-      store_rgb(out + (size_t)p * 3, v3(k.x, k.y, k.z));
-    }
-    const unsigned long long m = __ballot(hv);
-    int base = 0;
-    if (lane == 0 && m) base = atomicAdd(&counters[kHeavyCounter], __popcll(m));
-    base = __shfl(base, 0, 64);
-    if (hv) heavy[base + __popcll(m & lanemask_lt())] = j;
-  }
-}
+// Phase C after the resolver has finished (stream order: every carry-in is published).  A
+// workgroup takes a chunk of kChunk consecutive DEP entries: pass 1 (one lane per entry)
+// stores every clean entry (dep_fast, no level hit at its carry-in: its primary shade) and
+// compacts the others, with their carry-ins, into an LDS list; pass 2 shades that list in
+// full waves (levels 2.. with shading, shade_dep_cont; the whole pixel again when the scene
+// is not dep_fast).  Entries are independent once their carry-ins are known, so the list order
+// is free; the point is full waves of heavy work (~35 % of the entries are clean at quadric
+// 4096^2) without a second kernel or global atomics.
+constexpr int kChunk = 1024;
 
 template <bool kStage>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_FINISH_WAVES))) k_dep_heavy(
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_FINISH_WAVES))) k_dep_chunks(
     Scene sc, Cam cam, int W, int maxrec, const long long* __restrict__ dep_pix,
     const DepRec* __restrict__ deprec, const float4* __restrict__ pcol, CinG* __restrict__ cin,
-    const int* __restrict__ counters, const int* __restrict__ heavy,
-    uint8_t* __restrict__ out, unsigned long long* __restrict__ zcount, unsigned tag) {
+    const int* __restrict__ counters, uint8_t* __restrict__ out,
+    unsigned long long* __restrict__ zcount, TeamState* __restrict__ ts, unsigned tag) {
   __shared__ StageBuf<kStage> stage;
+  __shared__ int s_j[kChunk];
+  __shared__ float s_c[kChunk][3];
+  __shared__ int s_n;
   stage_scene<kStage>(sc, stage);
-  const int nh = counters[kHeavyCounter];
-  const int nb = (nh + 63) / 64;
-  const int lane = threadIdx.x & 63;
-  const int nw = (int)((gridDim.x * blockDim.x) >> 6);
+  const int ndep = counters[2];
+  const int nchunks = (ndep + kChunk - 1) / kChunk;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   int zero = 0;
-  for (int b = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6); b < nb; b += nw) {
-    const int k = b * 64 + lane;
-    if (k >= nh) continue;
-    const int j = heavy[k];
-    V3 c;
-    bool hit;
-    (void)cin_get(cin, j, tag, c, hit);   // published: k_dep_split checked every tag
-    const long long p = dep_pix[j];
-    V3 rgb;
-    if (sc.dep_fast) {
-      const float4 q = pcol[p];
-      rgb = shade_dep_cont(sc, deprec[p], maxrec, c, v3(q.x, q.y, q.z), zero);
-    } else {
-      const int y = (int)(p / W), x = (int)(p % W);
-      const V3 d = primary_dir(cam, x, y, zero);
-      PixelOut po;
-      shoot<kModeParityC>(sc, d, maxrec, c, po, zero);
-      rgb = po.rgb;
+  for (int ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
+    if (threadIdx.x == 0) s_n = 0;
+    __syncthreads();
+    for (int bb = wave; bb < kChunk / 64; bb += kBlock / 64) {
+      const int b = ch * (kChunk / 64) + bb;
+      if (b * 64 >= ndep) break;
+      const int j = b * 64 + lane;
+      V3 c = v3(0.0f, 0.0f, 0.0f);
+      bool hit = true;
+      (void)batch_carries(cin, ndep, b, tag, true, c, hit, ts);
+      const bool in = j < ndep;
+      const bool hv = in && (!sc.dep_fast || hit);
+      if (in && !hv) {
+        const long long p = dep_pix[j];
+        const float4 k = pcol[p];
+        store_rgb(out + (size_t)p * 3, v3(k.x, k.y, k.z));
+      }
+      const unsigned long long m = __ballot(hv);
+      int base = 0;
+      if (lane == 0 && m) base = atomicAdd(&s_n, __popcll(m));
+      base = __shfl(base, 0, 64);
+      if (hv) {
+        const int q = base + __popcll(m & lanemask_lt());
+        s_j[q] = j;
+        s_c[q][0] = c.x;
+        s_c[q][1] = c.y;
+        s_c[q][2] = c.z;
+      }
     }
-    store_rgb(out + (size_t)p * 3, rgb);
+    __syncthreads();
+    const int n = s_n;
+    for (int q = threadIdx.x; q < n; q += kBlock) {
+      const int j = s_j[q];
+      const V3 c = v3(s_c[q][0], s_c[q][1], s_c[q][2]);
+      const long long p = dep_pix[j];
+      V3 rgb;
+      if (sc.dep_fast) {
+        const float4 k = pcol[p];
+        rgb = shade_dep_cont(sc, deprec[p], maxrec, c, v3(k.x, k.y, k.z), zero);
+      } else {
+        const int y = (int)(p / W), x = (int)(p % W);
+        const V3 d = primary_dir(cam, x, y, zero);
+        PixelOut po;
+        shoot<kModeParityC>(sc, d, maxrec, c, po, zero);
+        rgb = po.rgb;
+      }
+      store_rgb(out + (size_t)p * 3, rgb);
+    }
+    __syncthreads();   // the list is rebuilt for the next chunk
   }
   flush_events(zero, zcount);
 }
@@ -1425,13 +1424,10 @@ static void enqueue_phase_c(const Scene& sc, const Cam& cam, bool st, int W, int
                        out,
                        zcount, (TeamState*)w.team, w.epoch, (w.side && w.split_shade) ? 1 : 0);
   } else {   // all of phase C after the resolver: clean entries, then full waves of the rest
-    hipLaunchKernelGGL(k_dep_split, dim3(w.phase_c_blocks), dim3(256), 0, stream, sc, w.dep_pix,
-                       (const float4*)w.wcarry, (CinG*)w.cin, w.counters, w.heavy, out,
-                       (TeamState*)w.team, w.epoch);
-    hipLaunchKernelGGL(st ? k_dep_heavy<true> : k_dep_heavy<false>, dim3(w.phase_c_blocks),
+    hipLaunchKernelGGL(st ? k_dep_chunks<true> : k_dep_chunks<false>, dim3(w.phase_c_blocks),
                        dim3(kBlock), 0, stream, sc, cam, W, maxrec, w.dep_pix,
                        (const DepRec*)w.deprec, (const float4*)w.wcarry, (CinG*)w.cin,
-                       w.counters, w.heavy, out, zcount, w.epoch);
+                       w.counters, out, zcount, (TeamState*)w.team, w.epoch);
   }
 }
 

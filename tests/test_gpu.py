@@ -62,8 +62,8 @@ def test_configs(key, scenes, table):
                                   "RC_NO_SIDE+RC_PHASE_C_FINISH"])
 def test_parity_schedules(knob, scenes, table, monkeypatch):
     """The parity pipeline's alternative schedules give the same bytes: phase C after the
-    resolver only (RC_NO_SIDE: clean entries, then full waves of the rest — k_dep_split /
-    k_dep_heavy; with RC_PHASE_C_FINISH through k_finish's batch claims), colours shaded
+    resolver only (RC_NO_SIDE: clean entries, then full waves of the rest — k_dep_chunks;
+    with RC_PHASE_C_FINISH through k_finish's batch claims), colours shaded
     beside the resolver (RC_SPLIT_SHADE), and no one-workgroup-per-CU reservation
     (RC_RESOLVE_SHARED, which also disables the side stream), and every first-bounce-miss
     pixel recomputed in phase C (RC_NO_DEP_FAST)."""
@@ -119,7 +119,7 @@ def test_zero_normalize_events(case, fast_dep, side, tmp_path, monkeypatch):
                     "radial-a0: 0.0125, position: [0, 0, -5]\n")
     if not fast_dep:
         monkeypatch.setenv("RC_NO_DEP_FAST", "1")
-    if not side:   # phase C after the resolver: k_dep_split / k_dep_heavy
+    if not side:   # phase C after the resolver: k_dep_chunks
         monkeypatch.setenv("RC_NO_SIDE", "1")
     s = rc.Scene.from_file(str(path))
     for w, h in ((1, 1), (2, 1), (3, 1), (1, 3)):
