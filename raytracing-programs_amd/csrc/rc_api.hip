@@ -73,9 +73,15 @@ struct FrameBufs {
 // streams, each resolver grid sized to A/kLanes CUs (one workgroup per CU), so the resolvers in
 // flight are always wholly resident side by side (a team spins on co-resident workgroups;
 // at most kLanes resolvers are in flight since each stream runs its resolvers in order).
-// Partition B runs every frame's phase A, compaction and phase C on per-slot streams.  A
-// resolver is latency-bound (its carry chains), so overlapping kLanes of them multiplies the
-// frame rate until partition B's pixel work becomes the bound.
+// Partition B runs the pixel phases: the frames' phase A one at a time in submission order
+// (each waits for the previous frame's, adone), so the frame whose resolver comes next always
+// has the whole partition; two streams (pix[0], pix[1]) alternate so a frame's compaction —
+// a chain of small latency-bound kernels — overlaps the next frame's phase A; each lane's
+// phase C runs on a stream of its own (pc[lane], after the frame's resolver); a slot's next
+// phase A waits for the slot's previous phase C (cdone).  A resolver is
+// latency-bound (its carry chains), so overlapping kLanes of them multiplies the frame rate
+// until partition B's pixel work becomes the bound.  (RC_PIPE_SLOTSTREAMS: the earlier form,
+// one stream per slot running A, compaction and C in turn.)
 struct Pipe {
   static constexpr int kSlots = 8;   // frame workspaces (a frame re-uses slot k after k's end)
   static constexpr int kLanes = 4;   // resolvers in flight (at most)
@@ -85,6 +91,11 @@ struct Pipe {
   int slots = 4;                     // workspaces / pixel streams in use (RC_PIPE_SLOTS)
   hipStream_t pix[kSlots] = {}, res[kLanes] = {};
   hipEvent_t ready[kSlots] = {}, done[kSlots] = {};
+  bool fifo = true;                  // pa = pix[0] + pc[] (false: RC_PIPE_SLOTSTREAMS)
+  hipStream_t pc[kLanes] = {};
+  hipEvent_t cdone[kSlots] = {};
+  bool cpend[kSlots] = {};           // slot k's phase C is enqueued and not yet synchronised
+  hipEvent_t adone[kSlots] = {};     // after slot k's phase A
   static constexpr int kEv = 64;     // resolver timing events of the last kEv frames
   hipEvent_t rt[kEv][2] = {};
   FrameBufs fb[kSlots];
@@ -541,11 +552,16 @@ void pipe_release_all() {
     (void)hipSetDevice(c.device);
     (void)hipDeviceSynchronize();
     for (int k = 0; k < p.slots; ++k) {
-      (void)hipStreamDestroy(p.pix[k]);
+      if (p.pix[k]) (void)hipStreamDestroy(p.pix[k]);
       (void)hipEventDestroy(p.ready[k]);
       (void)hipEventDestroy(p.done[k]);
+      (void)hipEventDestroy(p.cdone[k]);
+      (void)hipEventDestroy(p.adone[k]);
     }
-    for (int r = 0; r < p.lanes; ++r) (void)hipStreamDestroy(p.res[r]);
+    for (int r = 0; r < p.lanes; ++r) {
+      (void)hipStreamDestroy(p.res[r]);
+      if (p.pc[r]) (void)hipStreamDestroy(p.pc[r]);
+    }
     for (auto& e : p.rt) {
       (void)hipEventDestroy(e[0]);
       (void)hipEventDestroy(e[1]);
@@ -554,7 +570,7 @@ void pipe_release_all() {
   }
 }
 
-int pipe_init(DevCtx& c) {
+int pipe_init(DevCtx& c, long long pixels) {
   Pipe& p = c.pipe;
   if (p.init) return 0;
   static bool registered = false;
@@ -564,7 +580,12 @@ int pipe_init(DevCtx& c) {
   }
   // partition A: the low `res` bits of the CU mask, which the driver deals round-robin over
   // the XCDs (bit i -> XCD i mod 8), so both partitions span every XCD.
-  int res = c.cus / 2;
+  // Resolver partition: half the device for large images (quadric 4096^2: the carry chains
+  // need the waves), a quarter below 8 Mpixel, where the pixel phases are the bound (measured
+  // with frames in flight: reflection 2048^2 d4 6.9e9 -> 7.9e9, simple 1024^2 d6 3.5e9 ->
+  // 3.7e9 rays/s; quadric 4096^2 5.7e9 at 128 CUs vs 5.1e9 at 112).  Fixed at the first
+  // pipelined frame.
+  int res = pixels >= (8ll << 20) ? c.cus / 2 : c.cus / 4;
   if (const char* e = std::getenv("RC_PIPE_RES_CUS")) res = std::atoi(e);
   if (const char* e = std::getenv("RC_PIPE_RESOLVERS")) p.lanes = std::atoi(e);
   if (p.lanes < 1) p.lanes = 1;
@@ -573,18 +594,24 @@ int pipe_init(DevCtx& c) {
   if (p.slots < p.lanes + 1) p.slots = p.lanes + 1;
   if (p.slots > Pipe::kSlots) p.slots = Pipe::kSlots;
   p.rt_on = !std::getenv("RC_PIPE_NO_RT");
+  p.fifo = !std::getenv("RC_PIPE_SLOTSTREAMS");
   res = res / (8 * p.lanes) * (8 * p.lanes);   // whole CUs per XCD for every resolver
   if (res < 16 * p.lanes) res = 16 * p.lanes;
   if (res > c.cus - 16) res = (c.cus - 16) / (8 * p.lanes) * (8 * p.lanes);
   const int words = (c.cus + 31) / 32;
   std::vector<uint32_t> ma(words, 0), mb(words, 0);
   for (int i = 0; i < c.cus; ++i) (i < res ? ma : mb)[i / 32] |= 1u << (i % 32);
-  for (int r = 0; r < p.lanes; ++r)
+  for (int r = 0; r < p.lanes; ++r) {
     HIP_TRY(hipExtStreamCreateWithCUMask(&p.res[r], (uint32_t)words, ma.data()));
+    if (p.fifo) HIP_TRY(hipExtStreamCreateWithCUMask(&p.pc[r], (uint32_t)words, mb.data()));
+  }
   for (int k = 0; k < p.slots; ++k) {
-    HIP_TRY(hipExtStreamCreateWithCUMask(&p.pix[k], (uint32_t)words, mb.data()));
+    if (!p.fifo || k < 2)
+      HIP_TRY(hipExtStreamCreateWithCUMask(&p.pix[k], (uint32_t)words, mb.data()));
+    HIP_TRY(hipEventCreateWithFlags(&p.adone[k], hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&p.ready[k], hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&p.done[k], hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&p.cdone[k], hipEventDisableTiming));
   }
   for (auto& e : p.rt) {
     HIP_TRY(hipEventCreate(&e[0]));
@@ -611,7 +638,7 @@ int rc_frame_submit(const rc_scene* s, int W, int H, const rc_options* opt, uint
     c->pipe.frames++;
     return 0;
   }
-  if (pipe_init(*c)) return -1;
+  if (pipe_init(*c, (long long)W * H)) return -1;
   Pipe& p = c->pipe;
   const int k = (int)(p.total % p.slots);
   const int lane = (int)(p.total % p.lanes);
@@ -620,7 +647,9 @@ int rc_frame_submit(const rc_scene* s, int W, int H, const rc_options* opt, uint
   // and compaction take the whole device (then phase C returns to the slot's partition).
   // Slot k's previous frame is complete (rc_frames_wait synchronised every slot).
   const bool first = p.submitted == 0;
-  hipStream_t st = first ? c->stream : p.pix[k];
+  hipStream_t st = first ? c->stream : p.pix[p.fifo ? (int)(p.total & 1) : k];
+  if (p.fifo && p.cpend[k]) HIP_TRY(hipStreamWaitEvent(st, p.cdone[k], 0));
+  if (p.fifo && !first) HIP_TRY(hipStreamWaitEvent(st, p.adone[p.last], 0));
   rc::LaunchScene ls;
   if (upload_scene(b, st, s, ls) || b.zcount.ensure(64)) return -1;
   unsigned long long* zc = (unsigned long long*)b.zcount.p;
@@ -631,13 +660,20 @@ int rc_frame_submit(const rc_scene* s, int W, int H, const rc_options* opt, uint
     return -1;
   }
   w.rstream = p.res[lane];
-  w.pstream = first ? p.pix[k] : nullptr;
+  w.pstream = first ? p.pix[p.fifo ? 0 : k] : nullptr;
+  w.defer_c = p.fifo ? 1 : 0;
+  w.adone = p.fifo ? p.adone[k] : nullptr;
   w.rready = p.ready[k];
   w.rdone = p.done[k];
   const int e = (int)(p.submitted % Pipe::kEv);
   w.rt0 = p.rt_on ? p.rt[e][0] : nullptr;
   w.rt1 = p.rt_on ? p.rt[e][1] : nullptr;
   HIP_TRY(rc::launch_parity(ls, W, H, maxrec, d_out, w, zc, st, nullptr));
+  if (p.fifo) {   // phase C on the lane's stream, after the resolver
+    HIP_TRY(rc::launch_phase_c(ls, W, H, maxrec, d_out, w, zc, p.pc[lane]));
+    HIP_TRY(hipEventRecord(p.cdone[k], p.pc[lane]));
+    p.cpend[k] = true;
+  }
   p.submitted++;
   p.frames++;
   p.total++;
@@ -656,8 +692,12 @@ int rc_frames_wait(rc_timing* timing) {
   HIP_TRY(hipStreamSynchronize(c->stream));
   int rc = 0;
   if (p.init) {
-    for (int k = 0; k < p.slots; ++k) HIP_TRY(hipStreamSynchronize(p.pix[k]));
+    for (int k = 0; k < p.slots; ++k)
+      if (p.pix[k]) HIP_TRY(hipStreamSynchronize(p.pix[k]));
     for (int r = 0; r < p.lanes; ++r) HIP_TRY(hipStreamSynchronize(p.res[r]));
+    for (int r = 0; r < p.lanes; ++r)
+      if (p.pc[r]) HIP_TRY(hipStreamSynchronize(p.pc[r]));
+    for (int k = 0; k < p.slots; ++k) p.cpend[k] = false;
     for (int k = 0; k < p.slots; ++k) {   // the last frame of each slot
       if (!p.used[k] || !p.fb[k].team.p) continue;
       int err = 0;

@@ -1353,6 +1353,7 @@ hipError_t launch_parity(const LaunchScene& s, int W, int H, int maxrec, uint8_t
     hipLaunchKernelGGL(st ? k_phase_a<true> : k_phase_a<false>, grid, dim3(kBlock), 0, stream, sc, cam, W, H, maxrec, out,
                        w.cls, w.wcarry, (DepRec*)w.deprec, zcount);
   if (ev) (void)hipEventRecord(ev[0], stream);
+  if (w.adone) (void)hipEventRecord(w.adone, stream);
   (void)hipMemsetAsync(w.counters, 0, 16 * sizeof(int), stream);   // nseg, head, ndep, ...
   (void)hipMemsetAsync(w.team, 0, sizeof(TeamState), stream);     // error + round tags
   const int row_blocks = (H + kRowWaves - 1) / kRowWaves;
