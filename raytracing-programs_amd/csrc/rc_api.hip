@@ -235,6 +235,7 @@ int upload_scene(FrameBufs& b, hipStream_t stream, const rc_scene* s, rc::Launch
   ls.cam_h = h->cam_h;
   ls.refl_mask = 0;
   ls.has_quadric = 0;
+  ls.o0_ok = h->o0_ok && !std::getenv("RC_NO_O0");
   const rc_shape* hs = (const rc_shape*)((const char*)h + h->off_shapes);
   for (int k = 0; k < h->n && k < 64; ++k)
     if (hs[k].refl > 0.0f) ls.refl_mask |= 1ull << k;

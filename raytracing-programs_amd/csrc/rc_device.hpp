@@ -44,6 +44,7 @@ struct Scene {
   int n, m;
   unsigned long long refl_mask;          // bit k: shape k has reflectivity > 0 (k < 64)
   int has_quadric;                       // any quadric: picks the evaluator specialisation
+  int o0_ok;                             // primary rays may use rc_shape::o0 (nearest_primary)
   // Clean DEP entries (no bounce level hits at their carry-in) take their colour from phase
   // A's primary shade: set when every level's shade of such an entry is exactly zero (black
   // phantom, finite reflectivities; host check in upload_scene).
@@ -324,6 +325,86 @@ __device__ __forceinline__ int nearest(const Scene& sc, V3 O, V3 D, int skip, fl
   return idx;
 }
 
+// ------------------------------------------------------------------ primary rays --
+// The primary ray of every pixel starts at O = (0,0,0) (C/raycast.c:118-121).  Each test's
+// origin-only term is then a per-shape constant (rc_shape::o0, computed on the host by the
+// same operations at O = +0: bit-identical), and the quadric's b loses its O terms: with
+// finite coefficients each is a signed zero, and x + (+-0) = x for x != 0, so b equals
+// ((g*Dx + h*Dy) + i*Dz) up to the sign of a zero result — which no caller can see: b enters
+// disc only squared, a zero disc makes both roots +-0 (rejected by t > 0), and the linear
+// case's c / +-0 is +-inf or NaN (rejected by best > t / t > 0 alike).
+__device__ __forceinline__ bool hit_sphere_o0(V3 D, const rc_shape& s, RayK k, float& t) {
+  const V3 tv = v3(0.0f - s.p[0], 0.0f - s.p[1], 0.0f - s.p[2]);
+  float b = 2.0f * dot(D, tv);
+  float fac = k.a4 * s.o0;
+  float disc = (float)((double)b * (double)b - (double)fac);
+  if (disc < 0.0f) return false;
+  double sq = sqrt_ns((double)disc);
+  float tt = (float)(((double)(-b) - sq) / k.den);
+  if (tt < 0.0f) tt = (float)(((double)(-b) + sq) / k.den);
+  t = tt;
+  return true;
+}
+
+__device__ __forceinline__ bool hit_plane_o0(V3 D, const rc_shape& s, float& t) {
+  float den = dot(D, v3(s.n[0], s.n[1], s.n[2]));
+  if (den == 0.0f) return false;
+  float tt = (-s.o0) / den;
+  if (tt < 0.0f) return false;
+  t = tt;
+  return true;
+}
+
+__device__ __forceinline__ bool hit_quadric_o0(V3 D, const rc_shape& q, float& t) {
+  double acc;
+  acc = q.A * ((double)D.x * (double)D.x);
+  acc = acc + q.B * ((double)D.y * (double)D.y);
+  acc = acc + q.C * ((double)D.z * (double)D.z);
+  acc = acc + (double)(q.qd * D.x * D.y);
+  acc = acc + (double)(q.qe * D.x * D.z);
+  acc = acc + (double)(q.qf * D.y * D.z);
+  const float aq = (float)acc;
+  acc = (double)(q.qg * D.x);
+  acc = acc + (double)(q.qh * D.y);
+  acc = acc + (double)(q.qi * D.z);
+  const float bq = (float)acc;
+  const float cq = q.o0;
+  if ((double)aq == 0.0) {
+    t = (float)((-1.0 * (double)cq) / (double)bq);
+    return true;
+  }
+  const float disc = (float)((double)bq * (double)bq - 4.0 * (double)aq * (double)cq);
+  if ((double)disc < 0.0) return false;
+  const double den = 2.0 * (double)aq;
+  const double sq = sqrt_ns((double)disc);
+  float tt = (float)(((double)(-bq) - sq) / den);
+  if (tt <= 0.0f) tt = (float)(((double)(-bq) + sq) / den);
+  t = tt;
+  return true;
+}
+
+// nearest(sc, (0,0,0), D, -1, tbest) for a primary ray.
+__device__ __forceinline__ int nearest_primary(const Scene& sc, V3 D, float& tbest) {
+  if (!sc.o0_ok) return nearest(sc, v3(0.0f, 0.0f, 0.0f), D, -1, tbest);
+  const RayK rk = ray_consts(D);
+  float best = __builtin_inff();
+  int idx = -1;
+  for (int k = 0; k < sc.n; ++k) {
+    const rc_shape& s = sc.shapes[k];
+    float t = 0.0f;
+    bool hit = false;
+    if (s.type == RC_SHAPE_SPHERE) hit = hit_sphere_o0(D, s, rk, t);
+    else if (s.type == RC_SHAPE_PLANE) hit = hit_plane_o0(D, s, t);
+    else if (s.type == RC_SHAPE_QUADRIC) hit = hit_quadric_o0(D, s, t);
+    if (hit && best > t && t > 0.0f) {
+      best = t;
+      idx = k;
+    }
+  }
+  tbest = best;
+  return idx;
+}
+
 // C/raycast.c:441-531 (shadow_test = true): is any shape hit with 0 < t < inf?  The first
 // such shape is always accepted, so the loop may stop there.
 __device__ __forceinline__ bool shadowed(const Scene& sc, V3 O, V3 D, int skip) {
@@ -480,7 +561,7 @@ __device__ __forceinline__ void shoot(const Scene& sc, V3 d, int maxrec, V3 carr
   po.cls = kClsIdent;
   int zp = 0;   // events of the primary part (a DEP pixel's share of phase A)
   float t0;
-  const int i0 = nearest(sc, v3(0.0f, 0.0f, 0.0f), d, -1, t0);
+  const int i0 = nearest_primary(sc, d, t0);
   if (i0 < 0) return;                                   // C/raycast.c:328-331
   V3 P0, N0;
   hit_frame(sc, i0, v3(0.0f, 0.0f, 0.0f), d, t0, P0, N0, zp);

@@ -18,6 +18,7 @@ struct LaunchScene {
   float cam_w, cam_h;
   unsigned long long refl_mask;   // bit k: shape k reflective (n <= 64)
   int has_quadric;                // the scene has a quadric
+  int o0_ok;                      // primary rays may use rc_shape::o0
   int dep_fast;                   // clean DEP entries take phase A's primary shade (Scene)
 };
 

@@ -1309,6 +1309,7 @@ static Scene make_scene(const LaunchScene& s) {
   sc.m = s.m;
   sc.refl_mask = s.refl_mask;
   sc.has_quadric = s.has_quadric;
+  sc.o0_ok = s.o0_ok;
   sc.dep_fast = s.dep_fast;
   return sc;
 }

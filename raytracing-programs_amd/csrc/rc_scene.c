@@ -78,6 +78,45 @@ static void fill_shape(rc_shape *d, const shape_t *s) {
     d->qd = s->d; d->qe = s->e; d->qf = s->f;
     d->qg = s->g; d->qh = s->h; d->qi = s->i; d->qj = s->j;
   }
+  /* Origin-only terms of the intersection tests at O = (0,0,0), the primary rays' origin
+   * (C/raycast.c:118-121), by the device's operations in the same order (rc_device.hpp
+   * hit_sphere / hit_plane / hit_quadric with O = +0): sphere c (C/raycast.c:584-586),
+   * plane numerator (:550), quadric c (:626-638). */
+  const float ox = 0.0f, oy = 0.0f, oz = 0.0f;
+  const float tx = ox - d->p[0], ty = oy - d->p[1], tz = oz - d->p[2];
+  if (s->type == SPHERE) {
+    float dd = tx * tx;
+    dd = dd + ty * ty;
+    dd = dd + tz * tz;
+    d->o0 = (float)((double)dd - d->r2);
+  } else if (s->type == PLANE) {
+    float num = tx * d->n[0];
+    num = num + ty * d->n[1];
+    d->o0 = num + tz * d->n[2];
+  } else if (s->type == QUADRIC) {
+    double acc;
+    acc = d->A * ((double)ox * (double)ox);
+    acc = acc + d->B * ((double)oy * (double)oy);
+    acc = acc + d->C * ((double)oz * (double)oz);
+    acc = acc + (double)(d->qd * ox * oy);
+    acc = acc + (double)(d->qe * ox * oz);
+    acc = acc + (double)(d->qf * oy * oz);
+    acc = acc + (double)(d->qg * ox);
+    acc = acc + (double)(d->qh * oy);
+    acc = acc + (double)(d->qi * oz);
+    acc = acc + (double)d->qj;
+    d->o0 = (float)acc;
+  }
+}
+
+/* The primary-ray forms drop terms that are zero at O = 0 (rc_device.hpp nearest_primary);
+ * that holds for finite coefficients only. */
+static int o0_usable(const rc_shape *d) {
+  const float f[] = {d->p[0], d->p[1], d->p[2], d->n[0], d->n[1], d->n[2], d->qd, d->qe,
+                     d->qf, d->qg, d->qh, d->qi, d->qj, d->qa, d->qb, d->qc, d->o0};
+  for (unsigned k = 0; k < sizeof f / sizeof f[0]; k++)
+    if (!isfinite(f[k])) return 0;
+  return isfinite(d->r2) && isfinite(d->A) && isfinite(d->B) && isfinite(d->C);
 }
 
 static void fill_light(rc_light *d, const light_t *l) {
@@ -151,7 +190,11 @@ rc_packed_header *rc_pack_scene(const json_data_t *js) {
   rc_shape *ds = (rc_shape *)(buf + off_shapes);
   rc_light *dl = (rc_light *)(buf + off_lights);
   rc_shade_pair *dp = (rc_shade_pair *)(buf + off_pairs);
-  for (int k = 0; k < n; k++) fill_shape(&ds[k], sh[k]);
+  h->o0_ok = 1;
+  for (int k = 0; k < n; k++) {
+    fill_shape(&ds[k], sh[k]);
+    if (!o0_usable(&ds[k])) h->o0_ok = 0;
+  }
   fill_shape(&ds[n], &phantom);
   ds[n].type = -1;                       /* never intersected, only shaded */
   for (int k = 0; k < m; k++) fill_light(&dl[k], li[k]);

@@ -12,6 +12,7 @@
  * precomputed here with the identical IEEE operation (so the value is bit-identical):
  *   sphere  r*r in double (C/raycast.c:585), (float)(1.0/r) (C/raycast.c:465)
  *   quadric a,b,c widened to double (C/raycast.c:615-638, 504-517)
+ *   primary rays: the origin-only terms of each test at O = (0,0,0) (rc_shape::o0)
  *   shading opacity (float)((1.0-refl)-refr) (C/raycast.c:383) and the per (shape,light)
  *   colour products diffuse*light.color, specular*light.color (C/raycast.c:716-718,755-757)
  * Index n (one past the last shape) holds the phantom record shapes_list[-1].
@@ -44,7 +45,9 @@ typedef struct rc_shape {
   float qd, qe, qf;    /* quadric d, e, f                              */
   float qg, qh, qi, qj;/* quadric g, h, i, j                           */
   float qa, qb, qc;    /* quadric a, b, c (float)                      */
-  float pad0;
+  float o0;            /* primary rays (origin (0,0,0)): the origin-only */
+                       /* term, computed as the device would at O = 0:   */
+                       /* sphere c, plane numerator, quadric c          */
   double r2;           /* sphere (double)r*(double)r                   */
   double A, B, C;      /* quadric (double)a, (double)b, (double)c      */
   double pad1;
@@ -82,7 +85,8 @@ typedef struct rc_packed_header {
   int32_t off_pairs;
   int32_t bytes;        /* total image size                             */
   int32_t phantom_defined;
-  int32_t pad[7];
+  int32_t o0_ok;        /* every shape's o0 usable (finite coefficients) */
+  int32_t pad[6];
 } rc_packed_header;
 
 #ifdef __cplusplus
