@@ -241,7 +241,7 @@ static void o_shade(octx *c, float *out, int idx, const float *P, const float *N
     /* diffuse C/raycast.c:708-720 and specular C/raycast.c:733-758 */
     float dif[3] = {0, 0, 0}, spe[3] = {0, 0, 0};
     float th = o_dot(N, ld);
-    if (th > 0.0f) {
+    if (!(th <= 0.0)) {   /* C/raycast.c:713,740: a NaN theta is not <= 0 */
       for (int k = 0; k < 3; k++) dif[k] = (o->diffuse_color[k] * L->color[k]) * th;
       float view[3] = {D[0] * -1.0f, D[1] * -1.0f, D[2] * -1.0f};
       float r[3];

@@ -460,7 +460,6 @@ __device__ __forceinline__ V3 shade(const Scene& sc, int idx, V3 P, V3 N, V3 D, 
     V3 ld = v3(L.pos[0] - P.x, L.pos[1] - P.y, L.pos[2] - P.z);
     const float dist = length(ld);
     ld = normalize(ld, zero_events);
-    if (shadowed(sc, P, ld, skip)) continue;
     // radial attenuation C/raycast.c:666-669
     const float lin = L.r0 + L.r1 * dist;
     const float rad =
@@ -468,12 +467,12 @@ __device__ __forceinline__ V3 shade(const Scene& sc, int idx, V3 P, V3 N, V3 D, 
     // angular attenuation C/raycast.c:679-696.  v = normalize(P - L.pos): P - L.pos is -ld
     // component for component (round-to-nearest is sign-symmetric), so v = -ld and
     // alpha = -dot(ld, dir) exactly.  A zero-length ld (P on the light) is +0 in every
-    // component either way: then v = ld, and the reference counts a second zero event.
+    // component either way: then v = ld, and the reference counts a second zero event
+    // (only when the light is not shadowed: it is counted below, after the shadow test).
     float ang = 1.0f;
+    const bool z = dist == 0.0f;
     if (L.type == RC_LIGHT_SPOT) {
       const float a = dot(ld, v3(L.dir[0], L.dir[1], L.dir[2]));
-      const bool z = dist == 0.0f;
-      zero_events += z ? 1 : 0;
       const float alpha = z ? a : -a;
       if (alpha < L.cos_theta) {
         ang = 0.0f;
@@ -483,10 +482,20 @@ __device__ __forceinline__ V3 shade(const Scene& sc, int idx, V3 P, V3 N, V3 D, 
         ang = (float)pow((double)alpha, (double)L.a0);   // parity unpinned
       }
     }
+    const float th = dot(N, ld);
+    // A light behind the surface (th <= 0) contributes ((0 + 0) * rad) * ang = +-0 when rad
+    // and ang are finite, and out + (+-0) == out (out starts at +0 and a round-to-nearest
+    // sum is -0 only if both terms are): the reference's shadow ray (C/raycast.c:401-402)
+    // cannot change the colour then, so it is not traced.  P on a spot light (a counted
+    // zero-normalize event after the shadow test) keeps the test.
+    const bool inert = th <= 0.0f && __builtin_isfinite(rad) && __builtin_isfinite(ang) &&
+                       !(z && L.type == RC_LIGHT_SPOT);
+    if (inert) continue;
+    if (shadowed(sc, P, ld, skip)) continue;
+    if (L.type == RC_LIGHT_SPOT) zero_events += z ? 1 : 0;
     // diffuse C/raycast.c:708-720, specular C/raycast.c:733-758
     float dr = 0.0f, dg = 0.0f, db = 0.0f, sr = 0.0f, sg = 0.0f, sb = 0.0f;
-    const float th = dot(N, ld);
-    if (th > 0.0f) {
+    if (!(th <= 0.0f)) {   // C/raycast.c:713,740: a NaN theta is not <= 0
       const rc_shade_pair& p = pr[l];
       dr = p.dl[0] * th;
       dg = p.dl[1] * th;
