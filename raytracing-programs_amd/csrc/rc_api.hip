@@ -15,6 +15,7 @@
 
 #include <chrono>
 #include <cmath>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -122,6 +123,8 @@ struct DevCtx {
   hipEvent_t ev[kEvSets][5] = {};
   int prof_active = 0, prof_calls = 0, prof_parity = 0;
   DevBuf out;          // rc_render output pixmap
+  uint8_t* stage[2] = {nullptr, nullptr};   // pinned bounce buffers of copy_to_host
+  hipEvent_t stage_ev[2] = {nullptr, nullptr};
   FrameBufs fb;        // scene, counter and parity workspace of the plain path
   Pipe pipe;
   int resident_blocks = 0;
@@ -154,6 +157,114 @@ int ctx_get(int device, DevCtx** out) {
     c.init = true;
   }
   *out = &c;
+  return 0;
+}
+
+// ------------------------------------------------------------- device -> host copy --
+// The drop-in path ends with the image in the caller's pageable pixmap (C/raycast.c:52-53
+// mallocs it).  The runtime's own pageable copy stages through a bounce buffer and fills the
+// destination from one host thread (~3.2 ms for 4096^2 RGB).  copy_to_host streams 8 MiB
+// chunks into two pinned bounce buffers (DMA of chunk i+1 while chunk i is spread over host
+// threads) and copies each chunk out with a small persistent thread pool.
+constexpr size_t kStageChunk = 8u << 20;
+
+class CopyPool {
+ public:
+  static CopyPool& get() {   // never destroyed: its detached workers outlive main()
+    static CopyPool* pool = new CopyPool();
+    return *pool;
+  }
+  // memcpy(dst, src, n) split over the workers and the calling thread
+  void copy(uint8_t* dst, const uint8_t* src, size_t n) {
+    const int parts = nthreads_ + 1;
+    const size_t step = ((n + parts - 1) / parts + 4095) & ~(size_t)4095;
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      dst_ = dst;
+      src_ = src;
+      n_ = n;
+      step_ = step;
+      pending_ = nthreads_;
+      ++gen_;
+    }
+    cv_.notify_all();
+    const size_t len = n < step ? n : step;   // part 0
+    std::memcpy(dst, src, len);
+    std::unique_lock<std::mutex> lk(mu_);
+    done_.wait(lk, [&] { return pending_ == 0; });
+  }
+
+ private:
+  CopyPool() {
+    int t = 7;
+    if (const char* e = std::getenv("RC_COPY_THREADS")) t = std::atoi(e) - 1;
+    if (t < 0) t = 0;
+    if (t > 31) t = 31;
+    nthreads_ = t;
+    for (int i = 0; i < t; ++i) workers_.emplace_back([this, i] { run(i + 1); });
+    for (auto& w : workers_) w.detach();   // lives for the process
+  }
+  void run(int part) {
+    unsigned long long seen = 0;
+    for (;;) {
+      uint8_t* dst;
+      const uint8_t* src;
+      size_t n, step;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return gen_ != seen; });
+        seen = gen_;
+        dst = dst_;
+        src = src_;
+        n = n_;
+        step = step_;
+      }
+      const size_t off = (size_t)part * step;
+      if (off < n) std::memcpy(dst + off, src + off, n - off < step ? n - off : step);
+      std::unique_lock<std::mutex> lk(mu_);
+      if (--pending_ == 0) done_.notify_one();
+    }
+  }
+  std::mutex mu_;
+  std::condition_variable cv_, done_;
+  std::vector<std::thread> workers_;
+  int nthreads_ = 0;
+  unsigned long long gen_ = 0;
+  int pending_ = 0;
+  uint8_t* dst_ = nullptr;
+  const uint8_t* src_ = nullptr;
+  size_t n_ = 0, step_ = 0;
+};
+
+int copy_to_host(DevCtx& c, uint8_t* host, const uint8_t* dev, size_t bytes, hipStream_t st) {
+  if (std::getenv("RC_PLAIN_D2H")) {   // the runtime's pageable copy
+    HIP_TRY(hipMemcpyAsync(host, dev, bytes, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return 0;
+  }
+  for (int b = 0; b < 2; ++b) {
+    if (!c.stage[b]) {
+      HIP_TRY(hipHostMalloc((void**)&c.stage[b], kStageChunk, hipHostMallocDefault));
+      HIP_TRY(hipEventCreateWithFlags(&c.stage_ev[b], hipEventDisableTiming));
+    }
+  }
+  const size_t n = (bytes + kStageChunk - 1) / kStageChunk;
+  auto chunk = [&](size_t i) { return i + 1 < n ? kStageChunk : bytes - i * kStageChunk; };
+  for (size_t i = 0; i < 2 && i < n; ++i) {
+    HIP_TRY(hipMemcpyAsync(c.stage[i], dev + i * kStageChunk, chunk(i), hipMemcpyDeviceToHost,
+                           st));
+    HIP_TRY(hipEventRecord(c.stage_ev[i], st));
+  }
+  for (size_t i = 0; i < n; ++i) {
+    const int b = (int)(i & 1);
+    HIP_TRY(hipEventSynchronize(c.stage_ev[b]));
+    CopyPool::get().copy(host + i * kStageChunk, c.stage[b], chunk(i));
+    if (i + 2 < n) {
+      HIP_TRY(hipMemcpyAsync(c.stage[b], dev + (i + 2) * kStageChunk, chunk(i + 2),
+                             hipMemcpyDeviceToHost, st));
+      HIP_TRY(hipEventRecord(c.stage_ev[b], st));
+    }
+  }
   return 0;
 }
 
@@ -811,15 +922,30 @@ int rc_render(const rc_scene* s, int W, int H, const rc_options* opt, uint8_t* p
       rcodes[g] = -1;
       return;
     }
+    // The caller's pixmap is typically fresh from malloc (C/raycast.c:52-53): fault its pages
+    // in while the GPU renders, instead of inside the copy (every byte is overwritten).
+    if (!std::getenv("RC_NO_PREFAULT")) {
+      volatile uint8_t* p = pixmap + (size_t)g * row_bytes;
+      const size_t span = G == 1 ? (size_t)H * row_bytes : ((size_t)(nrows - 1) * G + 1) * row_bytes;
+      for (size_t o = 0; o < span; o += 4096) p[o] = 0;
+      if (span) p[span - 1] = 0;
+    }
     auto td = std::chrono::steady_clock::now();
-    hipError_t e = hipMemcpy2DAsync(pixmap + (size_t)g * row_bytes, row_bytes * G, d_out,
-                                    row_bytes, row_bytes, nrows, hipMemcpyDeviceToHost,
-                                    c->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-    if (e != hipSuccess) {
-      std::fprintf(stderr, "Error: HIP copy failed: %s\n", hipGetErrorString(e));
-      rcodes[g] = -1;
-      return;
+    if (G == 1) {   // contiguous image: staged, multi-threaded copy
+      if (copy_to_host(*c, pixmap, d_out, (size_t)H * row_bytes, c->stream)) {
+        rcodes[g] = -1;
+        return;
+      }
+    } else {
+      hipError_t e = hipMemcpy2DAsync(pixmap + (size_t)g * row_bytes, row_bytes * G, d_out,
+                                      row_bytes, row_bytes, nrows, hipMemcpyDeviceToHost,
+                                      c->stream);
+      if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+      if (e != hipSuccess) {
+        std::fprintf(stderr, "Error: HIP copy failed: %s\n", hipGetErrorString(e));
+        rcodes[g] = -1;
+        return;
+      }
     }
     if (check_spin_error(c->fb, opt)) {
       rcodes[g] = -1;
