@@ -187,6 +187,11 @@ int rc_render_device(const rc_scene *scene, int width, int height, int row0, int
 int rc_frame_submit(const rc_scene *scene, int width, int height, const rc_options *opt,
                     uint8_t *d_out);
 int rc_frames_wait(rc_timing *timing);
+/* Wait for every submitted frame, then release the current device's frame pipeline (its
+ * CU-partitioned streams and events; the frame workspaces stay allocated).  The next
+ * rc_frame_submit builds it again, re-reading RC_PIPE_* from the environment.  Returns what
+ * rc_frames_wait would. */
+int rc_pipe_reset(void);
 
 /* Duration (ms) of the last call's dominant kernel on the current device (the carry
  * resolver in parity mode, the render kernel otherwise), from HIP events on its stream. */

@@ -76,7 +76,8 @@ assert ctypes.sizeof(ShapeT) == 104 and ctypes.sizeof(LightT) == 72
 # the functions include/raycast_hip.h declares, per library
 HIP_EXPORTS = ["raycast", "rc_default_options", "rc_scene_create", "rc_scene_destroy",
                "rc_scene_parity_defined", "rc_render", "rc_render_device", "rc_last_kernel_ms",
-               "rc_profile_begin", "rc_profile_end", "rc_version"]
+               "rc_profile_begin", "rc_profile_end", "rc_version", "rc_frame_submit",
+               "rc_frames_wait", "rc_pipe_reset"]
 FRONT_EXPORTS = ["add_new_sphere", "add_new_plane", "add_new_quadric", "free_shape_list",
                  "free_light_list", "add_new_spot_light", "add_new_point_light", "parse_json",
                  "set_to_black", "ppm_WriteOutP3", "ppm_clamp"]
@@ -119,6 +120,7 @@ def hip_lib():
     lib.rc_frame_submit.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                     ctypes.POINTER(RcOptions), ctypes.c_void_p]
     lib.rc_frames_wait.argtypes = [ctypes.POINTER(RcTiming)]
+    lib.rc_pipe_reset.argtypes = []
     lib.rc_last_kernel_ms.restype = ctypes.c_double
     lib.rc_version.restype = ctypes.c_char_p
     lib.rc_default_options.argtypes = [ctypes.POINTER(RcOptions), ctypes.c_int]
@@ -264,6 +266,13 @@ def frames_wait(timing=None):
         raise RuntimeError("rc_frames_wait failed: a resolver hand-off timed out (see stderr)")
     if timing is not None:
         timing.update({k: getattr(t, k) for k, _ in RcTiming._fields_})
+
+
+def pipe_reset():
+    """Wait for every frame, then release the frame pipeline (rc_pipe_reset); the next
+    frame_submit rebuilds it from the current RC_PIPE_* environment."""
+    if hip_lib().rc_pipe_reset() != 0:
+        raise RuntimeError("rc_pipe_reset failed: a resolver hand-off timed out (see stderr)")
 
 
 def last_kernel_ms():

@@ -657,29 +657,39 @@ namespace {
 
 // Release the pipelines' CU-masked streams and events before the runtime's own teardown
 // (left to process exit they crash a profiled process's finalisation).
-void pipe_release_all() {
-  for (auto& c : g_ctx) {
-    Pipe& p = c.pipe;
-    if (!p.init) continue;
-    (void)hipSetDevice(c.device);
-    (void)hipDeviceSynchronize();
-    for (int k = 0; k < p.slots; ++k) {
-      if (p.pix[k]) (void)hipStreamDestroy(p.pix[k]);
-      (void)hipEventDestroy(p.ready[k]);
-      (void)hipEventDestroy(p.done[k]);
-      (void)hipEventDestroy(p.cdone[k]);
-      (void)hipEventDestroy(p.adone[k]);
-    }
-    for (int r = 0; r < p.lanes; ++r) {
-      (void)hipStreamDestroy(p.res[r]);
-      if (p.pc[r]) (void)hipStreamDestroy(p.pc[r]);
-    }
-    for (auto& e : p.rt) {
-      (void)hipEventDestroy(e[0]);
-      (void)hipEventDestroy(e[1]);
-    }
-    p.init = false;
+void pipe_release(DevCtx& c) {
+  Pipe& p = c.pipe;
+  if (!p.init) return;
+  (void)hipSetDevice(c.device);
+  (void)hipDeviceSynchronize();
+  for (int k = 0; k < p.slots; ++k) {
+    if (p.pix[k]) (void)hipStreamDestroy(p.pix[k]);
+    (void)hipEventDestroy(p.ready[k]);
+    (void)hipEventDestroy(p.done[k]);
+    (void)hipEventDestroy(p.cdone[k]);
+    (void)hipEventDestroy(p.adone[k]);
   }
+  for (int r = 0; r < p.lanes; ++r) {
+    (void)hipStreamDestroy(p.res[r]);
+    if (p.pc[r]) (void)hipStreamDestroy(p.pc[r]);
+  }
+  for (auto& e : p.rt) {
+    (void)hipEventDestroy(e[0]);
+    (void)hipEventDestroy(e[1]);
+  }
+  p.init = false;
+  p.submitted = 0;
+  p.frames = 0;
+  p.last = -1;
+  for (int k = 0; k < Pipe::kSlots; ++k) {
+    p.cpend[k] = false;
+    p.pix[k] = nullptr;
+  }
+  for (int r = 0; r < Pipe::kLanes; ++r) p.pc[r] = nullptr;
+}
+
+void pipe_release_all() {
+  for (auto& c : g_ctx) pipe_release(c);
 }
 
 int pipe_init(DevCtx& c, long long pixels) {
@@ -699,6 +709,8 @@ int pipe_init(DevCtx& c, long long pixels) {
   // pipelined frame.
   int res = pixels >= (8ll << 20) ? c.cus / 2 : c.cus / 4;
   if (const char* e = std::getenv("RC_PIPE_RES_CUS")) res = std::atoi(e);
+  p.lanes = 2;
+  p.slots = 4;
   if (const char* e = std::getenv("RC_PIPE_RESOLVERS")) p.lanes = std::atoi(e);
   if (p.lanes < 1) p.lanes = 1;
   if (p.lanes > Pipe::kLanes) p.lanes = Pipe::kLanes;
@@ -837,6 +849,16 @@ int rc_frames_wait(rc_timing* timing) {
   }
   p.frames = 0;
   p.submitted = 0;
+  return rc;
+}
+
+int rc_pipe_reset(void) {
+  int dev = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  DevCtx* c;
+  if (ctx_get(dev, &c)) return -1;
+  const int rc = rc_frames_wait(nullptr);
+  pipe_release(*c);
   return rc;
 }
 

@@ -197,11 +197,24 @@ def test_device_render_matches_host(scenes, table):
     np.testing.assert_array_equal(sh.cpu().numpy(), full[1::3])
 
 
-def test_frames_in_flight(scenes, table):
+PIPES = {"default": {},
+         "slot-streams": {"RC_PIPE_SLOTSTREAMS": "1"},
+         "three-lanes": {"RC_PIPE_RESOLVERS": "3", "RC_PIPE_RES_CUS": "144", "RC_PIPE_SLOTS": "6"},
+         "one-lane-small-a": {"RC_PIPE_RESOLVERS": "1", "RC_PIPE_RES_CUS": "32",
+                              "RC_PIPE_NO_RT": "1"},
+         "one-wg-per-cu": {"RC_RESOLVE_LDS_KB": "96", "RC_TEAM_BLOCKS": "24"}}
+
+
+@pytest.mark.parametrize("pipe", list(PIPES))
+def test_frames_in_flight(pipe, scenes, table, monkeypatch):
     """rc_frame_submit: consecutive frames overlap on two CU partitions (the resolver of one
     beside the pixel phases of the next); every frame is still byte-identical.  Mixed scenes,
-    sizes and modes exercise the slot workspaces' re-use and re-upload."""
+    sizes and modes exercise the slot workspaces' re-use and re-upload; the pipeline is
+    rebuilt (rc_pipe_reset) under each partition / stream layout."""
     torch = pytest.importorskip("torch")
+    for k, v in PIPES[pipe].items():
+        monkeypatch.setenv(k, v)
+    rc.pipe_reset()
     seq = ["quadric:4096x4096:d6:parity", "reflection:2048x2048:d4:parity",
            "quadric:4096x4096:d6:parity", "simple:1024x1024:d6:parity",
            "quadric:1024x1024:d6:fast", "quadric:512x384:d6:parity",
@@ -221,6 +234,8 @@ def test_frames_in_flight(scenes, table):
             rc.frame_submit(scenes[scene], w, h, buf.data_ptr(), depth=d, mode=mode)
         tim = {}
         rc.frames_wait(tim)
-        assert tim["resolve_ms"] > 0.0
+        assert tim["resolve_ms"] > 0.0 or "RC_PIPE_NO_RT" in PIPES[pipe]
         for key, scene, w, h, d, mode, buf in jobs:
-            assert p3_md5(buf.cpu().numpy()) == table[key]["md5"], key
+            assert p3_md5(buf.cpu().numpy()) == table[key]["md5"], (pipe, key)
+    monkeypatch.undo()
+    rc.pipe_reset()   # later tests get the default pipeline
