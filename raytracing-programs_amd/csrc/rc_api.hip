@@ -176,6 +176,7 @@ class CopyPool {
   }
   // memcpy(dst, src, n) split over the workers and the calling thread
   void copy(uint8_t* dst, const uint8_t* src, size_t n) {
+    std::lock_guard<std::mutex> one_at_a_time(call_mu_);   // concurrent rc_render callers
     const int parts = nthreads_ + 1;
     const size_t step = ((n + parts - 1) / parts + 4095) & ~(size_t)4095;
     {
@@ -225,7 +226,7 @@ class CopyPool {
       if (--pending_ == 0) done_.notify_one();
     }
   }
-  std::mutex mu_;
+  std::mutex mu_, call_mu_;
   std::condition_variable cv_, done_;
   std::vector<std::thread> workers_;
   int nthreads_ = 0;
@@ -528,7 +529,10 @@ int check_spin_error(FrameBufs& b, const rc_options* opt) {
 
 double event_ms(hipEvent_t a, hipEvent_t b) {
   float ms = 0.0f;
-  if (hipEventElapsedTime(&ms, a, b) != hipSuccess) return 0.0;
+  if (hipEventElapsedTime(&ms, a, b) != hipSuccess) {
+    (void)hipGetLastError();   // not sticky: later launches check hipGetLastError()
+    return 0.0;
+  }
   return ms;
 }
 
