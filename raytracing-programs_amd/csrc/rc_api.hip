@@ -449,6 +449,10 @@ int ensure_parity(DevCtx& c, FrameBufs& b, int W, int H, rc::ParityWork& w, int 
   // The team spins on a counter barrier: its blocks (the first of the grid) and the grid as
   // a whole must be co-resident, so the grid never exceeds the resident capacity.
   w.resolve_blocks = c.resident_blocks / c.cus * res_cus;   // whole CUs' worth
+  if (const char* e = std::getenv("RC_RESOLVE_GRID")) {     // experiments: a smaller grid
+    const int g = std::atoi(e);
+    if (g >= 8 && g < w.resolve_blocks) w.resolve_blocks = g;
+  }
   w.resolve_lds = c.resident_lds;
   // team size: 128 of a whole-device grid; 3/8 of a pipelined resolver's grid (64 -> 24:
   // measured 4.77e9 vs 4.50e9 rays/s at 32, 4.49e9 at 20)
