@@ -710,12 +710,12 @@ int pipe_init(DevCtx& c, long long pixels) {
   }
   // partition A: the low `res` bits of the CU mask, which the driver deals round-robin over
   // the XCDs (bit i -> XCD i mod 8), so both partitions span every XCD.
-  // Resolver partition: half the device for large images (quadric 4096^2: the carry chains
-  // need the waves), a quarter below 8 Mpixel, where the pixel phases are the bound (measured
-  // with frames in flight: reflection 2048^2 d4 6.9e9 -> 7.9e9, simple 1024^2 d6 3.5e9 ->
-  // 3.7e9 rays/s; quadric 4096^2 5.7e9 at 128 CUs vs 5.1e9 at 112).  Fixed at the first
-  // pipelined frame.
-  int res = pixels >= (8ll << 20) ? c.cus / 2 : c.cus / 4;
+  // Resolver partition by image size, fixed at the first pipelined frame (measured with frames
+  // in flight, scripts/pipe_sweep.sh): a quarter of the CUs below 8 Mpixel, where the pixel
+  // phases are the bound (reflection 2048^2 d4 6.9e9 -> 7.9e9, simple 1024^2 d6 3.5e9 -> 3.7e9
+  // rays/s vs half); half up to 32 Mpixel (quadric 4096^2: 5.7e9 at 128 CUs, 5.1e9 at 112);
+  // 3/8 above (quadric 8192^2: 7.4e9 at 96 CUs, 6.4e9 at 128, 6.0e9 at 80).
+  int res = pixels < (8ll << 20) ? c.cus / 4 : pixels < (32ll << 20) ? c.cus / 2 : c.cus * 3 / 8;
   if (const char* e = std::getenv("RC_PIPE_RES_CUS")) res = std::atoi(e);
   p.lanes = 2;
   p.slots = 4;
