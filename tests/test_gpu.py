@@ -239,3 +239,58 @@ def test_frames_in_flight(pipe, scenes, table, monkeypatch):
             assert p3_md5(buf.cpu().numpy()) == table[key]["md5"], (pipe, key)
     monkeypatch.undo()
     rc.pipe_reset()   # later tests get the default pipeline
+
+
+LIGHT = ("light, color: [1.5, 1.2, 1.0], radial-a2: 0.01, radial-a1: 0.0125, radial-a0: 0.0125, "
+         "position: [3, 6, 1]\n")
+DEGENERATE = {
+    "no-shapes": LIGHT,
+    "no-lights": "sphere, radius: 1.0, diffuse_color: [1, 0, 0], specular_color: [1, 1, 1], "
+                 "position: [0, 0, -5], reflectivity: 0.5, refractivity: 0, ior: 1\n",
+    "matte-only": "sphere, radius: 1.0, diffuse_color: [1, 0, 0], specular_color: [1, 1, 1], "
+                  "position: [0, 0, -5], reflectivity: 0, refractivity: 0, ior: 1\n"
+                  "plane, normal: [0, 1, 0], diffuse_color: [0.3, 0.3, 0.3], "
+                  "position: [0, -1, 0], reflectivity: 0\n" + LIGHT,
+    "mirror-box": "".join(
+        f"plane, normal: [{n}], diffuse_color: [0.4, 0.5, 0.6], specular_color: [1, 1, 1], "
+        f"position: [{p}], reflectivity: 0.9\n"
+        for n, p in (("0, 1, 0", "0, -2, 0"), ("0, -1, 0", "0, 2, 0"), ("1, 0, 0", "-2, 0, 0"),
+                     ("-1, 0, 0", "2, 0, 0"), ("0, 0, 1", "0, 0, -8"))) + LIGHT,
+    "lone-mirror-plane": "plane, normal: [0, 0.6, 0.8], diffuse_color: [0.2, 0.7, 0.3], "
+                         "specular_color: [1, 1, 1], position: [0, 0, -6], reflectivity: 1.0\n"
+                         + LIGHT,
+    "full-reflect-sphere": "sphere, radius: 2.0, diffuse_color: [0, 0, 1], specular_color: "
+                           "[1, 1, 1], position: [0, 0, -6], reflectivity: 1.0, refractivity: 0, "
+                           "ior: 1\n" + LIGHT,
+}
+
+
+@pytest.mark.parametrize("case", list(DEGENERATE))
+def test_degenerate_scenes(case, tmp_path):
+    """Edge scenes against the oracle, every depth class and mode, one frame at a time and
+    with frames in flight: no shapes, no lights, nothing reflective (no carry at all), a
+    closed mirror box (deep bounce chains), a lone mirror plane and a perfect mirror sphere
+    (every first bounce misses: the image is one long carry segment)."""
+    torch = pytest.importorskip("torch")
+    path = tmp_path / f"{case}.scene"
+    path.write_text("camera, width: 2.0, height: 2.0\n" + DEGENERATE[case])
+    s = rc.Scene.from_file(str(path))
+    bufs = []
+    for w, h in ((64, 48), (7, 5)):
+        for d in (0, 1, 4, 6):
+            for mode in ("parity", "fast"):
+                want, st = oracle_render(s, w, h, d, mode)
+                if not st["parity_defined"]:
+                    continue
+                np.testing.assert_array_equal(rc.render(s, w, h, depth=d, mode=mode), want,
+                                              err_msg=f"{case} {w}x{h} d{d} {mode}")
+                buf = torch.empty((h, w, 3), dtype=torch.uint8, device="cuda")
+                bufs.append((buf, want, f"{case} {w}x{h} d{d} {mode} in flight"))
+    torch.cuda.synchronize()
+    for buf, want, msg in bufs:
+        h, w, _ = want.shape
+        d = int(msg.split(" d")[1].split()[0])
+        rc.frame_submit(s, w, h, buf.data_ptr(), depth=d, mode=msg.split()[3])
+    rc.frames_wait()
+    for buf, want, msg in bufs:
+        np.testing.assert_array_equal(buf.cpu().numpy(), want, err_msg=msg)
