@@ -421,13 +421,56 @@ struct WinStats {
   int lane, coop, changers;
 };
 
+// Carry predictor for dense runs.  Inside a run of changers the carry creeps: at quadric
+// 4096^2 the seven 1 377-entry all-changer segments move one component by a near-constant
+// number of float ulps per entry (9-12, 143-156, -195..-209, ...) and keep the other two.
+// The cooperative evaluator then spends its spare lane groups on entry pos+1 at guessed
+// carry-ins bits(c) + mean delta of the last few changes (+-1, +-2.. ulps on the moving
+// component); when entry pos's exact output equals a guess bit for bit, entry pos+1's
+// evaluation at that guess IS its exact evaluation and two entries retire in one step.  The
+// guesses only choose what to evaluate, never what is accepted.
+struct CarryHist {
+  V3 h[4];   // carries after the last changes, h[0] the latest
+  int n;
+};
+#ifndef RC_PREDICT
+#define RC_PREDICT 1
+#endif
+constexpr bool kPredict = RC_PREDICT != 0;
+__device__ __forceinline__ void hist_push(CarryHist& hs, V3 c) {
+  hs.h[3] = hs.h[2];
+  hs.h[2] = hs.h[1];
+  hs.h[1] = hs.h[0];
+  hs.h[0] = c;
+  hs.n = hs.n < 4 ? hs.n + 1 : 4;
+}
+// guess q (1..) of the carry after c: the mean delta of the history, in float bits, with the
+// moving component offset by 0, -1, +1, -2, +2, ...
+__device__ __forceinline__ V3 hist_guess(const CarryHist& hs, V3 c, int q) {
+  const V3 o = hs.h[hs.n - 1];
+  const int m = hs.n - 1;
+  auto md = [&](float a, float b) {
+    const int d = (int)(__float_as_uint(a) - __float_as_uint(b));
+    return (d + (d >= 0 ? m / 2 : -(m / 2))) / m;
+  };
+  int dx = md(hs.h[0].x, o.x), dy = md(hs.h[0].y, o.y), dz = md(hs.h[0].z, o.z);
+  const int off = (q & 1) ? -((q + 1) >> 1) : (q >> 1);   // q = 1, 2, 3, 4.. -> 0, -1, +1, -2..
+  const int ax = abs(dx), ay = abs(dy), az = abs(dz);
+  if (ax >= ay && ax >= az) dx += q == 1 ? 0 : off;
+  else if (ay >= az) dy += q == 1 ? 0 : off;
+  else dz += q == 1 ? 0 : off;
+  return v3(__uint_as_float(__float_as_uint(c.x) + (unsigned)dx),
+            __uint_as_float(__float_as_uint(c.y) + (unsigned)dy),
+            __uint_as_float(__float_as_uint(c.z) + (unsigned)dz));
+}
+
 __device__ __forceinline__ int wave_window(const Scene& sc, int maxrec,
                                            const DepRec* __restrict__ deprec,
                                            const long long* __restrict__ dep_pix, int base,
                                            int end, V3& c, V3& mine, bool& mhit,
                                            const LaneShape& ls,
                                            int G, bool& dense, bool& changed,
-                                           WinStats& ws, int K
+                                           WinStats& ws, int K, CarryHist& hs
 #if RC_STAMPS
                                            , Stamps* st_
 #endif
@@ -464,6 +507,7 @@ __device__ __forceinline__ int wave_window(const Scene& sc, int maxrec,
           mine = c;
           mhit = h;
         }
+        hs.n = 0;
         pos = nvalid;
         break;
       }
@@ -472,7 +516,9 @@ __device__ __forceinline__ int wave_window(const Scene& sc, int maxrec,
         mine = c;
         mhit = h;
       }
+      if (k > 0 || hs.n == 0) hs.n = 0, hist_push(hs, c);   // the run starts at this change
       c = v3(__shfl(o.x, k, 64), __shfl(o.y, k, 64), __shfl(o.z, k, 64));
+      hist_push(hs, c);
       pos = k + 1;
       changed = true;
       ++ws.changers;
@@ -481,15 +527,19 @@ __device__ __forceinline__ int wave_window(const Scene& sc, int maxrec,
       continue;
     }
     ++ws.coop;
-    const int i = pos + e;
+    // predictive step (CarryHist): group 0 takes entry pos at c, the others entry pos+1 at
+    // guessed carry-ins; otherwise groups take entries pos, pos+1, .. all at c
+    const bool predict = hs.n >= 2 && E >= 2 && pos + 1 < nvalid && kPredict;
+    const int i = predict ? pos + (e > 0 ? 1 : 0) : pos + e;
+    const V3 ce = (predict && e > 0 && e < E) ? hist_guess(hs, c, e) : c;
     const bool act = e < E && i < nvalid;
     const DepRec ri = shfl_rec(r, i < 64 ? i : 63);
-    V3 oc = c;
+    V3 oc = ce;
     bool hg = false;
 #if RC_STAMPS
-#define RC_SPEC1(GT, Q) carry_path_spec<GT, Q>(sc, ls, kself, G, half, ri, maxrec, c, zero, hg, st_)
+#define RC_SPEC1(GT, Q) carry_path_spec<GT, Q>(sc, ls, kself, G, half, ri, maxrec, ce, zero, hg, st_)
 #else
-#define RC_SPEC1(GT, Q) carry_path_spec<GT, Q>(sc, ls, kself, G, half, ri, maxrec, c, zero, hg)
+#define RC_SPEC1(GT, Q) carry_path_spec<GT, Q>(sc, ls, kself, G, half, ri, maxrec, ce, zero, hg)
 #endif
 #define RC_SPEC(GT) (sc.has_quadric ? RC_SPEC1(GT, true) : RC_SPEC1(GT, false))
     if (act) {
@@ -497,15 +547,59 @@ __device__ __forceinline__ int wave_window(const Scene& sc, int maxrec,
       else if (G == 4) oc = RC_SPEC(4);
       else if (G == 16) oc = RC_SPEC(16);
       else if (spec) oc = RC_SPEC(0);
-      else oc = carry_path_coop(sc, ls, kself, G, ri, maxrec, c, zero, hg);
+      else oc = carry_path_coop(sc, ls, kself, G, ri, maxrec, ce, zero, hg);
     }
 #undef RC_SPEC
 #undef RC_SPEC1
+    if (predict) {
+      const V3 o0 = v3(__shfl(oc.x, 0, 64), __shfl(oc.y, 0, 64), __shfl(oc.z, 0, 64));
+      const bool h0 = __shfl((int)hg, 0, 64) != 0;
+      if (lane == pos) {
+        mine = c;
+        mhit = h0;
+      }
+      if (same_bits(o0, c)) {   // entry pos leaves the carry: the run is over
+        hs.n = 0;
+        pos += 1;
+        if (++clean_run >= K) coop = false;
+        continue;
+      }
+      changed = true;
+      ++ws.changers;
+      clean_run = 0;
+      hist_push(hs, o0);
+      const unsigned long long mm =
+          __ballot(act && e > 0 && (lane % GE) == 0 && same_bits(ce, o0));
+      if (mm == 0) {
+        c = o0;
+        pos += 1;
+        continue;
+      }
+      const int gl = __ffsll((long long)mm) - 1;   // leader lane of the matching group
+      const V3 o1 = v3(__shfl(oc.x, gl, 64), __shfl(oc.y, gl, 64), __shfl(oc.z, gl, 64));
+      const bool h1 = __shfl((int)hg, gl, 64) != 0;
+      if (lane == pos + 1) {
+        mine = o0;
+        mhit = h1;
+      }
+      pos += 2;
+      if (same_bits(o1, o0)) {
+        hs.n = 0;
+        c = o0;
+        if (++clean_run >= K) coop = false;
+      } else {
+        ++ws.changers;
+        hist_push(hs, o1);
+        c = o1;
+      }
+      continue;
+    }
     const unsigned long long mc = __ballot(act && (lane % GE) == 0 && !same_bits(oc, c));
     // entry pos+q's hit flag sits in its group's first lane, q*GE
     const int q = lane - pos;
     const bool hq = __shfl((int)hg, (q >= 0 && q < E ? q : 0) * GE, 64) != 0;
     if (mc == 0) {
+      hs.n = 0;
       const int lim = pos + E < nvalid ? pos + E : nvalid;
       if (lane >= pos && lane < lim) {
         mine = c;
@@ -520,7 +614,9 @@ __device__ __forceinline__ int wave_window(const Scene& sc, int maxrec,
       mine = c;
       mhit = hq;
     }
+    if (g > 0 || hs.n == 0) hs.n = 0, hist_push(hs, c);
     c = v3(__shfl(oc.x, g * GE, 64), __shfl(oc.y, g * GE, 64), __shfl(oc.z, g * GE, 64));
+    hist_push(hs, c);
     pos += g + 1;
     changed = true;
     ++ws.changers;
@@ -996,12 +1092,14 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
     V3 c = seg_init_carry(seg_key, wcarry, s);
     bool dense = false;
     WinStats ws = {0, 0, 0};
+    CarryHist hs;
+    hs.n = 0;
     for (int j = start; j < end; j += 64) {
       V3 mine;
       bool mhit, changed;
       iters += wave_window(sc, maxrec, deprec, dep_pix, j, end, c, mine, mhit, ls, G, dense,
                            changed, ws,
-                           wave_k
+                           wave_k, hs
 #if RC_STAMPS
                            , &stp
 #endif
