@@ -460,6 +460,11 @@ int ensure_parity(DevCtx& c, FrameBufs& b, int W, int H, rc::ParityWork& w, int 
   if (const char* e = std::getenv("RC_TEAM_BLOCKS")) w.team_blocks = std::atoi(e);
   if (w.team_blocks > 256) w.team_blocks = 256;
   if (w.team_blocks > w.resolve_blocks / 2) w.team_blocks = w.resolve_blocks / 2;
+  // helper blocks for handed-off dense runs (k_resolve): 8 of the grid
+  w.helpers = std::getenv("RC_HELPERS") ? std::atoi(std::getenv("RC_HELPERS")) : 8;
+  if (w.helpers < 0) w.helpers = 0;
+  if (w.team_blocks + w.helpers > w.resolve_blocks * 3 / 4) w.helpers = 0;
+  w.hand_run = std::getenv("RC_HAND_RUN") ? std::atoi(std::getenv("RC_HAND_RUN")) : 512;
   w.long_len = std::getenv("RC_LONG_LEN") ? std::atoi(std::getenv("RC_LONG_LEN")) : 32768;
   w.wave_k = std::getenv("RC_WAVE_K") ? std::atoi(std::getenv("RC_WAVE_K")) : 2;
   w.resolve_k = std::getenv("RC_RESOLVE_K") ? std::atoi(std::getenv("RC_RESOLVE_K")) : 1;

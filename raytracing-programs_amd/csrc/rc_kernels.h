@@ -49,6 +49,8 @@ struct ParityWork {
   int resolve_blocks;       // persistent resolver grid (<= resident capacity)
   int resolve_lds;          // dynamic LDS per resolver block (occupancy control)
   int team_blocks;          // workgroups in the long-segment team (0: no team)
+  int helpers;              // workgroups taking handed-off dense runs (0: none)
+  int hand_run;             // changes in a row before a regular wave hands its run off
   int long_len;             // segments with >= long_len entries go to the team
   int phase_c_blocks;       // grid-stride phase C grid
   int phase_c_finish;       // phase C after the resolver through k_finish's claims (RC_PHASE_C_FINISH)

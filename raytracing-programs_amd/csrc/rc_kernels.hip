@@ -432,12 +432,14 @@ struct WinStats {
 struct CarryHist {
   V3 h[4];   // carries after the last changes, h[0] the latest
   int n;
+  int run;   // changes in a row (a hand-off to a helper block starts a long run, k_resolve)
 };
 #ifndef RC_PREDICT
 #define RC_PREDICT 1
 #endif
 constexpr bool kPredict = RC_PREDICT != 0;
 __device__ __forceinline__ void hist_push(CarryHist& hs, V3 c) {
+  hs.run = hs.n == 0 ? 0 : hs.run + 1;
   hs.h[3] = hs.h[2];
   hs.h[2] = hs.h[1];
   hs.h[1] = hs.h[0];
@@ -454,11 +456,12 @@ __device__ __forceinline__ V3 hist_guess(const CarryHist& hs, V3 c, int q) {
     return (d + (d >= 0 ? m / 2 : -(m / 2))) / m;
   };
   int dx = md(hs.h[0].x, o.x), dy = md(hs.h[0].y, o.y), dz = md(hs.h[0].z, o.z);
-  const int off = (q & 1) ? -((q + 1) >> 1) : (q >> 1);   // q = 1, 2, 3, 4.. -> 0, -1, +1, -2..
+  const int j = q - 1;
+  const int off = (j & 1) ? -((j + 1) >> 1) : (j >> 1);   // q = 1, 2, 3, 4.. -> 0, -1, +1, -2..
   const int ax = abs(dx), ay = abs(dy), az = abs(dz);
-  if (ax >= ay && ax >= az) dx += q == 1 ? 0 : off;
-  else if (ay >= az) dy += q == 1 ? 0 : off;
-  else dz += q == 1 ? 0 : off;
+  if (ax >= ay && ax >= az) dx += off;
+  else if (ay >= az) dy += off;
+  else dz += off;
   return v3(__uint_as_float(__float_as_uint(c.x) + (unsigned)dx),
             __uint_as_float(__float_as_uint(c.y) + (unsigned)dy),
             __uint_as_float(__float_as_uint(c.z) + (unsigned)dz));
@@ -718,13 +721,21 @@ struct BlockWinShared {
   uint8_t hit[kResolveBlock];   // per entry: some level hit at the window's carry
   int wpos[2][4];
   float wout[2][4][3];
+  // predictive steps (helper blocks): per group its output, hit flag and guess
+  float pout[16][3];
+  float pce[16][3];
+  int phit[16];
+  int pmatch;
 };
 
+// hp (helper blocks): carry predictor; the cooperative step then takes entry pos at c in
+// group 0 and entry pos+1 at Eb-1 guessed carry-ins in the other groups (wave_window's
+// predictive step with the whole block: 15 guesses instead of 3).
 __device__ __forceinline__ void block_window(const Scene& sc, int maxrec, BlockWinShared& bw,
                                              int base, int nvalid, V3& c, const LaneShape& ls,
                                              int G, bool& dense, bool& changed, int K,
                                              CinG* __restrict__ cin, unsigned tag,
-                                             WinStats& ws) {
+                                             WinStats& ws, CarryHist* hp = nullptr) {
   constexpr int kNo = 0x7fffffff;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   changed = false;
@@ -742,6 +753,71 @@ __device__ __forceinline__ void block_window(const Scene& sc, int maxrec, BlockW
     int last;      // entries [pos, last] resolve with carry c
     V3 cn = c;
     bool hit;
+    if (coop && hp && kPredict && hp->n >= 2 && pos + 1 < nvalid && Eb <= 16 && Eb >= 2) {
+      ++ws.coop;
+      const int gi = wave * E + e;
+      const int i = pos + (gi > 0 ? 1 : 0);
+      const V3 ce = gi > 0 ? hist_guess(*hp, c, gi) : c;
+      const DepRec ri = bw.rec[i];
+      V3 oc = ce;
+      bool hg = false;
+#define RC_SPEC1(GT, Q) carry_path_spec<GT, Q>(sc, ls, kself, G, half, ri, maxrec, ce, zero, hg)
+#define RC_SPEC(GT) (sc.has_quadric ? RC_SPEC1(GT, true) : RC_SPEC1(GT, false))
+      if (G == 8) oc = RC_SPEC(8);
+      else if (G == 4) oc = RC_SPEC(4);
+      else if (G == 16) oc = RC_SPEC(16);
+      else oc = RC_SPEC(0);
+#undef RC_SPEC
+#undef RC_SPEC1
+      if ((lane % GE) == 0) {
+        bw.pout[gi][0] = oc.x;
+        bw.pout[gi][1] = oc.y;
+        bw.pout[gi][2] = oc.z;
+        bw.pce[gi][0] = ce.x;
+        bw.pce[gi][1] = ce.y;
+        bw.pce[gi][2] = ce.z;
+        bw.phit[gi] = hg ? 1 : 0;
+      }
+      __syncthreads();
+      const V3 o0 = v3(bw.pout[0][0], bw.pout[0][1], bw.pout[0][2]);
+      if (wave == 0) {
+        const bool mt = lane > 0 && lane < Eb &&
+                        same_bits(v3(bw.pce[lane][0], bw.pce[lane][1], bw.pce[lane][2]), o0);
+        const unsigned long long mm = __ballot(mt);
+        if (lane == 0) bw.pmatch = mm ? __ffsll((long long)mm) - 1 : 0;
+      }
+      __syncthreads();
+      const int mi = bw.pmatch;
+      if (t == pos) cin_put(cin, base + pos, c, tag, bw.phit[0] != 0);
+      if (same_bits(o0, c)) {   // entry pos leaves the carry: the run is over
+        hp->n = 0;
+        pos += 1;
+        if (++clean_run >= K) coop = false;
+      } else {
+        changed = true;
+        ++ws.changers;
+        clean_run = 0;
+        hist_push(*hp, o0);
+        if (mi > 0) {
+          const V3 o1 = v3(bw.pout[mi][0], bw.pout[mi][1], bw.pout[mi][2]);
+          if (t == pos + 1) cin_put(cin, base + pos + 1, o0, tag, bw.phit[mi] != 0);
+          pos += 2;
+          if (same_bits(o1, o0)) {
+            hp->n = 0;
+            c = o0;
+          } else {
+            ++ws.changers;
+            hist_push(*hp, o1);
+            c = o1;
+          }
+        } else {
+          c = o0;
+          pos += 1;
+        }
+      }
+      __syncthreads();   // pout / pmatch are rewritten by the next step
+      continue;
+    }
     if (!coop) {
       ++ws.lane;
       const bool act = t >= pos && t < nvalid;
@@ -808,6 +884,13 @@ __device__ __forceinline__ void block_window(const Scene& sc, int maxrec, BlockW
       last = coop ? (pos + Eb < nvalid ? pos + Eb : nvalid) - 1 : nvalid - 1;
     }
     if (t >= pos && t <= last) cin_put(cin, base + t, c, tag, bw.hit[t] != 0);
+    if (hp) {   // keep the predictor's history across the non-predictive steps
+      if (!hit || last > pos) hp->n = 0;
+      if (hit) {
+        if (hp->n == 0) hist_push(*hp, c);
+        hist_push(*hp, cn);
+      }
+    }
     pos = last + 1;
     c = cn;
     par ^= 1;
@@ -833,10 +916,25 @@ struct alignas(32) TeamSlot {
   unsigned long long g[4];
 };
 
+// Dense-run hand-off (k_resolve helper blocks): a regular wave deep in a run of changers
+// hands the rest of its segment (position, carry, predictor history) to a helper block.
+constexpr int kDenseQ = 64;
+constexpr int kHandMin = 256;    // entries left in the segment
+struct DenseItem {
+  int s, j, hn, ready;
+  float c[3];
+  float h[4][3];
+};
+struct DenseQueue {
+  int prod, claim, finished;     // hand-offs, helper claims, regular-loop waves done
+  int pad[29];
+  DenseItem item[kDenseQ];
+};
 struct TeamState {
   int error;        // a granule spin timed out (5 s)
   int pad[31];
   TeamSlot slot[2][kTeamMax];
+  DenseQueue dq;
 };
 
 __device__ __forceinline__ void team_publish(TeamState* ts, int round, unsigned pos, V3 c) {
@@ -884,7 +982,8 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
     const int* __restrict__ seg_start, const int* __restrict__ seg_order,
     int* __restrict__ counters, int* __restrict__ head,
     CinG* __restrict__ cin, int team_blocks, int long_len, TeamState* __restrict__ ts,
-    unsigned* __restrict__ trace, int G, int wave_k, int resolve_k, unsigned tag) {
+    unsigned* __restrict__ trace, int G, int wave_k, int resolve_k, unsigned tag,
+    int helpers, int hand_run) {
   // census for phase C's side kernel: it only proceeds once every resolver block is resident
   if (threadIdx.x == 0)
     __hip_atomic_fetch_add(&counters[5], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -915,6 +1014,7 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
     if (ls.has) ls.s = sc.shapes[kself];
   }
 
+  __shared__ BlockWinShared s_bw;   // the team leader's and the helpers' block windows
   if ((int)blockIdx.x < team_blocks) {
     // ------------------------------------------------------------------- team --
     // Changers inside long segments come in dense clusters separated by long clean runs
@@ -929,7 +1029,6 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
     //            back to the team.
     __shared__ int s_pos[4];
     __shared__ float s_o[4][3];
-    __shared__ BlockWinShared s_bw;
     __shared__ int s_gpos;
     __shared__ float s_nc[3];
     const int T = team_blocks;
@@ -1076,6 +1175,72 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
     // on is independent; a frame without long segments gets the whole grid)
   }
 
+  // ------------------------------------------------------------- helper blocks --
+  // Blocks [team_blocks, team_blocks + helpers) take the runs regular waves hand off (below)
+  // and resolve the rest of each such segment with block windows and 15 carry guesses per
+  // step.  They leave once every regular-loop wave is done and no hand-off is pending.
+  if ((int)blockIdx.x >= team_blocks && (int)blockIdx.x < team_blocks + helpers) {
+    __shared__ int s_item;
+    const int total = ((int)gridDim.x - helpers) * (kResolveBlock / 64);
+    const int t = threadIdx.x;
+    for (;;) {
+      if (t == 0) {
+        const int k = atomicAdd(&ts->dq.claim, 1);
+        int got = -1;
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        if (k < kDenseQ) {
+          for (;;) {
+            if (__hip_atomic_load(&ts->dq.item[k].ready, __ATOMIC_ACQUIRE,
+                                  __HIP_MEMORY_SCOPE_AGENT)) {
+              got = k;
+              break;
+            }
+            if (__hip_atomic_load(&ts->dq.finished, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >=
+                    total &&
+                __hip_atomic_load(&ts->dq.prod, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <= k)
+              break;   // every regular wave is done and nobody produced item k
+            if (__builtin_amdgcn_s_memrealtime() - t0 > 500000000ull) {   // 5 s
+              __hip_atomic_store(&ts->error, 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              break;
+            }
+            __builtin_amdgcn_s_sleep(8);
+          }
+        }
+        s_item = got;
+      }
+      __syncthreads();
+      const int k = s_item;
+      if (k < 0) break;
+      const DenseItem& it = ts->dq.item[k];
+      const int sg = it.s;
+      int j = it.j;
+      V3 c = v3(it.c[0], it.c[1], it.c[2]);
+      CarryHist hs;
+      hs.n = it.hn;
+      hs.run = hand_run;
+      for (int q = 0; q < 4; ++q) hs.h[q] = v3(it.h[q][0], it.h[q][1], it.h[q][2]);
+      const int end = (sg + 1 < nseg) ? seg_start[sg + 1] : ndep;
+      bool dense = true;
+      WinStats hws = {0, 0, 0};
+      if (j + t < end) s_bw.rec[t] = rec_at(deprec, dep_pix, j + t);
+      __syncthreads();
+      while (j < end) {
+        const int nv = end - j < kResolveBlock ? end - j : kResolveBlock;
+        DepRec nxt;
+        const int jn = j + nv;
+        if (jn + t < end) nxt = rec_at(deprec, dep_pix, jn + t);
+        bool changed;
+        block_window(sc, maxrec, s_bw, j, nv, c, ls, G, dense, changed, resolve_k, cin, tag,
+                     hws, &hs);
+        j = jn;
+        __syncthreads();   // everyone is done reading this window's records
+        if (j + t < end) s_bw.rec[t] = nxt;
+        __syncthreads();
+      }
+    }
+    return;   // helpers take no regular segments
+  }
+
   // ------------------------------------------------------------- regular waves --
   for (;;) {
     int s = 0;
@@ -1094,6 +1259,7 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
     WinStats ws = {0, 0, 0};
     CarryHist hs;
     hs.n = 0;
+    hs.run = 0;
     for (int j = start; j < end; j += 64) {
       V3 mine;
       bool mhit, changed;
@@ -1105,6 +1271,31 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
 #endif
                            );
       if (j + lane < end) cin_put(cin, j + lane, mine, tag, mhit);
+      // a long run of changers: hand the rest of the segment to a helper block (15 carry
+      // guesses per step instead of this wave's 3)
+      if (helpers > 0 && hs.run >= hand_run && hs.n >= 2 && end - (j + 64) >= kHandMin) {
+        int k = 0;
+        if (lane == 0) k = atomicAdd(&ts->dq.prod, 1);
+        k = __shfl(k, 0, 64);
+        if (k < kDenseQ) {
+          if (lane == 0) {
+            DenseItem& it = ts->dq.item[k];
+            it.s = s;
+            it.j = j + 64;
+            it.hn = hs.n;
+            it.c[0] = c.x;
+            it.c[1] = c.y;
+            it.c[2] = c.z;
+            for (int q = 0; q < 4; ++q) {
+              it.h[q][0] = hs.h[q].x;
+              it.h[q][1] = hs.h[q].y;
+              it.h[q][2] = hs.h[q].z;
+            }
+            __hip_atomic_store(&it.ready, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+          }
+          break;
+        }
+      }
     }
 #if RC_STAMPS
     if (trace && lane == 0 && end - start > 1000) {
@@ -1120,6 +1311,9 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
       trace[3 * (size_t)ndep + 4 * (size_t)nseg + 8 * 8192 + s] = (unsigned)t_seg;
     }
   }
+  // this wave hands nothing off any more (helper blocks wait for every such wave)
+  if (lane == 0)
+    __hip_atomic_fetch_add(&ts->dq.finished, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ------------------------------------------------------------------ parity phase C --
@@ -1481,7 +1675,7 @@ hipError_t launch_parity(const LaunchScene& s, int W, int H, int maxrec, uint8_t
                      maxrec, (const DepRec*)w.deprec, w.dep_pix, w.seg_key, w.wcarry,
                      w.seg_start, w.seg_order, w.counters, w.counters + 1, (CinG*)w.cin, w.team_blocks,
                      w.long_len, (TeamState*)w.team, w.trace, w.coop_group, w.wave_k,
-                     w.resolve_k, w.epoch);
+                     w.resolve_k, w.epoch, w.helpers, w.hand_run);
   if (w.rstream) {
     if (w.rt1) (void)hipEventRecord(w.rt1, rs);
     (void)hipEventRecord(w.rdone, rs);

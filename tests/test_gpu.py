@@ -59,15 +59,18 @@ def test_configs(key, scenes, table):
 
 @pytest.mark.parametrize("knob", ["RC_NO_SIDE", "RC_SPLIT_SHADE", "RC_RESOLVE_SHARED",
                                   "RC_NO_DEP_FAST", "RC_NO_SIDE+RC_NO_DEP_FAST",
-                                  "RC_NO_SIDE+RC_PHASE_C_FINISH", "RC_NO_O0"])
+                                  "RC_NO_SIDE+RC_PHASE_C_FINISH", "RC_NO_O0", "RC_HAND_RUN",
+                                  "RC_HELPERS"])
 def test_parity_schedules(knob, scenes, table, monkeypatch):
     """The parity pipeline's alternative schedules give the same bytes: phase C after the
     resolver only (RC_NO_SIDE: clean entries, then full waves of the rest — k_dep_chunks;
     with RC_PHASE_C_FINISH through k_finish's batch claims), colours shaded
     beside the resolver (RC_SPLIT_SHADE), and no one-workgroup-per-CU reservation
     (RC_RESOLVE_SHARED, which also disables the side stream), and every first-bounce-miss
-    pixel recomputed in phase C (RC_NO_DEP_FAST), and primary rays through the general
-    intersection tests instead of the origin-zero forms (RC_NO_O0)."""
+    pixel recomputed in phase C (RC_NO_DEP_FAST), primary rays through the general
+    intersection tests instead of the origin-zero forms (RC_NO_O0), a hand-off to the helper
+    blocks after every change (RC_HAND_RUN=1: the queue overflows) and a single helper block
+    (RC_HELPERS=1)."""
     for k in knob.split("+"):
         monkeypatch.setenv(k, "1")
     for key in ("quadric:4096x4096:d6:parity", "reflection:2048x2048:d4:parity",
