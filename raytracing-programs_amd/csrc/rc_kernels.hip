@@ -1181,6 +1181,7 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
   // step.  They leave once every regular-loop wave is done and no hand-off is pending.
   if ((int)blockIdx.x >= team_blocks && (int)blockIdx.x < team_blocks + helpers) {
     __shared__ int s_item;
+    __shared__ DenseItem s_it;
     const int total = ((int)gridDim.x - helpers) * (kResolveBlock / 64);
     const int t = threadIdx.x;
     for (;;) {
@@ -1195,7 +1196,10 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
               got = k;
               break;
             }
-            if (__hip_atomic_load(&ts->dq.finished, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >=
+            // Acquire on `finished` (released by each wave after its last possible hand-off)
+            // makes every slot claim those waves made visible: only then does prod <= k
+            // prove that item k never comes.
+            if (__hip_atomic_load(&ts->dq.finished, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) >=
                     total &&
                 __hip_atomic_load(&ts->dq.prod, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <= k)
               break;   // every regular wave is done and nobody produced item k
@@ -1207,11 +1211,12 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
           }
         }
         s_item = got;
+        if (got >= 0) s_it = ts->dq.item[got];   // after the acquire on `ready`
       }
       __syncthreads();
       const int k = s_item;
       if (k < 0) break;
-      const DenseItem& it = ts->dq.item[k];
+      const DenseItem& it = s_it;
       const int sg = it.s;
       int j = it.j;
       V3 c = v3(it.c[0], it.c[1], it.c[2]);
