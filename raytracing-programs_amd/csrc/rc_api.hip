@@ -463,6 +463,7 @@ int ensure_parity(DevCtx& c, FrameBufs& b, int W, int H, rc::ParityWork& w, int 
   // helper blocks for handed-off dense runs (k_resolve): 8 of the grid
   w.helpers = std::getenv("RC_HELPERS") ? std::atoi(std::getenv("RC_HELPERS")) : 8;
   if (w.helpers < 0) w.helpers = 0;
+  if (w.helpers > rc::kDenseSlots) w.helpers = rc::kDenseSlots;   // one ring slot per helper
   if (w.team_blocks + w.helpers > w.resolve_blocks * 3 / 4) w.helpers = 0;
   w.hand_run = std::getenv("RC_HAND_RUN") ? std::atoi(std::getenv("RC_HAND_RUN")) : 512;
   w.long_len = std::getenv("RC_LONG_LEN") ? std::atoi(std::getenv("RC_LONG_LEN")) : 32768;
@@ -525,15 +526,58 @@ int enqueue_render(DevCtx& c, const rc_scene* s, int W, int H, int row0, int row
 
 // After a synchronised parity render: the resolver's and phase C's bounded spins set
 // TeamState.error (first word) if a hand-off never completed; the image is then invalid.
+// The report names the first spin that failed (TeamState: code, workgroup, site detail), the
+// helper queue's counters and, for a missing carry-in, the segment it belongs to and how many
+// entries of the frame were never published.
+int report_spin_error(const FrameBufs& b, const char* where) {
+  int e[4] = {0, 0, 0, 0};
+  if (hipMemcpy(e, b.team.p, sizeof e, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  if (!e[0]) return 0;
+  static const char* site[] = {"", "team granule", "phase-C carry-in", "helper queue"};
+  int dq[3] = {0, 0, 0}, cnt[16] = {};
+  (void)hipMemcpy(dq, (const char*)b.team.p + rc::team_dq_offset(), sizeof dq,
+                  hipMemcpyDeviceToHost);
+  (void)hipMemcpy(cnt, b.counters.p, sizeof cnt, hipMemcpyDeviceToHost);
+  std::fprintf(stderr,
+               "Error: parity resolver hand-off timed out (code %d: %s; %s) at workgroup %d, "
+               "detail %d/%d; segments %d, DEP entries %d, resolver census %d, helper queue "
+               "prod %d claim %d finished %d, side workgroups go %d gave-up %d\n",
+               e[0], e[0] >= 1 && e[0] <= 3 ? site[e[0]] : "?", where, e[1], e[2], e[3], cnt[0],
+               cnt[2], cnt[5], dq[0], dq[1], dq[2], cnt[12], cnt[13]);
+  const int nseg = cnt[0], ndep = cnt[2];
+  if (nseg > 0 && ndep > 0 && b.cin.p && b.seg_start.p) {
+    std::vector<int> starts(nseg);
+    std::vector<unsigned long long> g((size_t)ndep * 3);
+    if (hipMemcpy(starts.data(), b.seg_start.p, starts.size() * sizeof(int),
+                  hipMemcpyDeviceToHost) == hipSuccess &&
+        hipMemcpy(g.data(), b.cin.p, g.size() * sizeof(unsigned long long),
+                  hipMemcpyDeviceToHost) == hipSuccess) {
+      long long missing = 0;
+      int shown = 0;
+      for (int s = 0; s < nseg; ++s) {
+        const int end = s + 1 < nseg ? starts[s + 1] : ndep;
+        int first = -1, n = 0;
+        for (int j = starts[s]; j < end; ++j) {
+          const unsigned t0 = (unsigned)(g[3 * (size_t)j] >> 32) & 0x7fffffffu;
+          if (t0 != b.epoch) {
+            if (first < 0) first = j;
+            ++n;
+          }
+        }
+        missing += n;
+        if (n && shown++ < 8)
+          std::fprintf(stderr, "  segment %d [%d, %d) length %d: %d entries unpublished from %d\n",
+                       s, starts[s], end, end - starts[s], n, first);
+      }
+      std::fprintf(stderr, "  %lld of %d carry-ins unpublished\n", missing, ndep);
+    }
+  }
+  return -1;
+}
+
 int check_spin_error(FrameBufs& b, const rc_options* opt) {
   if (!(opt->mode == RC_MODE_PARITY && opt->max_recursion > 1) || !b.team.p) return 0;
-  int err = 0;
-  if (hipMemcpy(&err, b.team.p, sizeof err, hipMemcpyDeviceToHost) != hipSuccess) return -1;
-  if (err) {
-    std::fprintf(stderr, "Error: parity resolver hand-off timed out (code %d)\n", err);
-    return -1;
-  }
-  return 0;
+  return report_spin_error(b, "one frame");
 }
 
 double event_ms(hipEvent_t a, hipEvent_t b) {
@@ -837,12 +881,7 @@ int rc_frames_wait(rc_timing* timing) {
     for (int k = 0; k < p.slots; ++k) p.cpend[k] = false;
     for (int k = 0; k < p.slots; ++k) {   // the last frame of each slot
       if (!p.used[k] || !p.fb[k].team.p) continue;
-      int err = 0;
-      HIP_TRY(hipMemcpy(&err, p.fb[k].team.p, sizeof err, hipMemcpyDeviceToHost));
-      if (err) {
-        std::fprintf(stderr, "Error: parity resolver hand-off timed out (code %d)\n", err);
-        rc = -1;
-      }
+      if (report_spin_error(p.fb[k], "frames in flight")) rc = -1;
     }
     const int n = !p.rt_on ? 0 : p.submitted < Pipe::kEv ? (int)p.submitted : Pipe::kEv;
     double sum = 0.0;

@@ -71,7 +71,8 @@ struct ParityWork {
 
 constexpr int kSegOrderMax = 65536;   // segments ordered for the resolver queue (else FIFO)
 constexpr int kCinBytes = 24;         // one carry-in = three tagged 8-byte granules
-constexpr int kLdsShapesMax = 64;     // k_resolve stages up to this many shapes in LDS
+constexpr int kLdsShapesMax = 64;
+constexpr int kDenseSlots = 64;       // k_resolve's hand-off ring (helper workgroups at most)     // k_resolve stages up to this many shapes in LDS
 
 hipError_t launch_render(const LaunchScene& s, int W, int H, int row0, int row_step, int nrows,
                          int maxrec, uint8_t* out, unsigned long long* zcount,
@@ -88,6 +89,7 @@ hipError_t launch_phase_c(const LaunchScene& s, int W, int H, int maxrec, uint8_
 size_t deprec_bytes();
 size_t row_stats_bytes();
 size_t team_state_bytes();
+size_t team_dq_offset();   // DenseQueue {prod, claim, finished} inside TeamState
 int resolve_blocks_resident(int cus, int lds_bytes);
 int side_lds_bytes(int resolve_dyn_lds);
 int phase_c_side_blocks(int cus, int side_lds);

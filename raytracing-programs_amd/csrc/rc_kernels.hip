@@ -917,25 +917,57 @@ struct alignas(32) TeamSlot {
 };
 
 // Dense-run hand-off (k_resolve helper blocks): a regular wave deep in a run of changers
-// hands the rest of its segment (position, carry, predictor history) to a helper block.
-constexpr int kDenseQ = 64;
+// hands the rest of its segment (position, carry, predictor history) to a helper block — but
+// only to one that is idle: a helper announces itself (idle += 1) before it claims the next
+// item, and a wave hands off only after taking one such announcement (idle -= 1), so every
+// item has a helper already waiting for it and nothing queues behind a busy helper (a queued
+// run would sit on the critical path; quadric 8192^2 has more dense runs than helpers).  At
+// most `helpers` items are outstanding, so item k lives in ring slot k % kDenseQ, tagged k+1.
+constexpr int kDenseQ = kDenseSlots;   // ring slots (>= helpers, checked by the host)
 constexpr int kHandMin = 256;    // entries left in the segment
 struct DenseItem {
-  int s, j, hn, ready;
+  int s, j, hn, ready;           // ready = item index + 1 once published
   float c[3];
   float h[4][3];
 };
 struct DenseQueue {
-  int prod, claim, finished;     // hand-offs, helper claims, regular-loop waves done
-  int pad[29];
+  int prod, claim, finished, idle;   // hand-offs, helper claims, regular-loop waves done,
+  int pad[28];                       // idle helper announcements not yet taken
   DenseItem item[kDenseQ];
 };
 struct TeamState {
-  int error;        // a granule spin timed out (5 s)
-  int pad[31];
+  // First bounded spin that timed out (first writer wins, rc_spin_error): code (1 team
+  // granule, 2 phase-C carry-in, 3 helper queue), the workgroup and a site detail.  Once it is
+  // set every other spin gives up at its next check instead of waiting out its own limit.
+  int error;
+  int err_block;
+  int err_info;
+  int err_info2;
+  int pad[28];
   TeamSlot slot[2][kTeamMax];
   DenseQueue dq;
 };
+
+constexpr unsigned long long kSpinLimit = 500000000ull;   // 5 s of the 100 MHz clock
+constexpr unsigned long long kSpinPoll = 100000ull;       // check the error word after 1 ms
+
+__device__ __forceinline__ void set_error(TeamState* ts, int code, int info, int info2) {
+  int expect = 0;
+  if (__hip_atomic_compare_exchange_strong(&ts->error, &expect, code, __ATOMIC_RELAXED,
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+    __hip_atomic_store(&ts->err_block, (int)blockIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&ts->err_info, info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&ts->err_info2, info2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+// A spin that started at t0 gives up: its own limit passed, or (after 1 ms) another spin
+// already failed.
+__device__ __forceinline__ bool spin_expired(TeamState* ts, unsigned long long t0) {
+  const unsigned long long dt = __builtin_amdgcn_s_memrealtime() - t0;
+  if (dt > kSpinLimit) return true;
+  return dt > kSpinPoll &&
+         __hip_atomic_load(&ts->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+}
 
 __device__ __forceinline__ void team_publish(TeamState* ts, int round, unsigned pos, V3 c) {
   TeamSlot* sl = &ts->slot[round & 1][blockIdx.x];
@@ -967,8 +999,8 @@ __device__ __forceinline__ bool team_collect(TeamState* ts, int round, int b, un
              __uint_as_float((unsigned)g3));
       return true;
     }
-    if (__builtin_amdgcn_s_memrealtime() - t0 > 500000000ull) {
-      __hip_atomic_store(&ts->error, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (spin_expired(ts, t0)) {
+      set_error(ts, 1, round, b);
       return false;
     }
   }
@@ -1186,32 +1218,37 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
     const int t = threadIdx.x;
     for (;;) {
       if (t == 0) {
+        __hip_atomic_fetch_add(&ts->dq.idle, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const int k = atomicAdd(&ts->dq.claim, 1);
+        DenseItem& slot = ts->dq.item[k % kDenseQ];
         int got = -1;
-        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-        if (k < kDenseQ) {
-          for (;;) {
-            if (__hip_atomic_load(&ts->dq.item[k].ready, __ATOMIC_ACQUIRE,
-                                  __HIP_MEMORY_SCOPE_AGENT)) {
-              got = k;
-              break;
-            }
-            // Acquire on `finished` (released by each wave after its last possible hand-off)
-            // makes every slot claim those waves made visible: only then does prod <= k
-            // prove that item k never comes.
-            if (__hip_atomic_load(&ts->dq.finished, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) >=
-                    total &&
-                __hip_atomic_load(&ts->dq.prod, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <= k)
-              break;   // every regular wave is done and nobody produced item k
-            if (__builtin_amdgcn_s_memrealtime() - t0 > 500000000ull) {   // 5 s
-              __hip_atomic_store(&ts->error, 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              break;
-            }
-            __builtin_amdgcn_s_sleep(8);
+        // the limit measures a lack of progress: it restarts whenever a regular wave
+        // finishes or hands a run off
+        unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        int seen = -1;
+        for (;;) {
+          if (__hip_atomic_load(&slot.ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == k + 1) {
+            got = k;
+            break;
           }
+          // Acquire on `finished` (released by each wave after its last possible hand-off)
+          // makes every item those waves produced visible: only then does prod <= k prove
+          // that item k never comes.
+          const int fin =
+              __hip_atomic_load(&ts->dq.finished, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+          const int prod = __hip_atomic_load(&ts->dq.prod, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (fin >= total && prod <= k) break;   // every regular wave is done, no item k
+          if (fin + prod != seen) {
+            seen = fin + prod;
+            t0 = __builtin_amdgcn_s_memrealtime();
+          } else if (spin_expired(ts, t0)) {
+            set_error(ts, 3, k, fin);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(8);
         }
         s_item = got;
-        if (got >= 0) s_it = ts->dq.item[got];   // after the acquire on `ready`
+        if (got >= 0) s_it = slot;   // after the acquire on `ready`
       }
       __syncthreads();
       const int k = s_item;
@@ -1279,12 +1316,18 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
       // a long run of changers: hand the rest of the segment to a helper block (15 carry
       // guesses per step instead of this wave's 3)
       if (helpers > 0 && hs.run >= hand_run && hs.n >= 2 && end - (j + 64) >= kHandMin) {
-        int k = 0;
-        if (lane == 0) k = atomicAdd(&ts->dq.prod, 1);
+        int k = -1;
+        if (lane == 0 &&
+            __hip_atomic_load(&ts->dq.idle, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > 0) {
+          if (__hip_atomic_fetch_add(&ts->dq.idle, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > 0)
+            k = atomicAdd(&ts->dq.prod, 1);
+          else   // lost the race for the last idle helper: give the announcement back
+            __hip_atomic_fetch_add(&ts->dq.idle, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         k = __shfl(k, 0, 64);
-        if (k < kDenseQ) {
+        if (k >= 0) {
           if (lane == 0) {
-            DenseItem& it = ts->dq.item[k];
+            DenseItem& it = ts->dq.item[k % kDenseQ];
             it.s = s;
             it.j = j + 64;
             it.hn = hs.n;
@@ -1296,7 +1339,7 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
               it.h[q][1] = hs.h[q].y;
               it.h[q][2] = hs.h[q].z;
             }
-            __hip_atomic_store(&it.ready, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&it.ready, k + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
           }
           break;
         }
@@ -1350,9 +1393,10 @@ __device__ __forceinline__ bool batch_carries(CinG* cin, int ndep, int b, unsign
     if (j < ndep) ok = cin_get(cin, j, tag, c, hit);
     if (__all(ok)) return true;
     if (!wait) return false;
-    if (__builtin_amdgcn_s_memrealtime() - t0 > 500000000ull) {   // 5 s
-      if ((threadIdx.x & 63) == 0)
-        __hip_atomic_store(&ts->error, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (spin_expired(ts, t0)) {
+      // the first entry of the batch that is still missing
+      const unsigned long long miss = __ballot(!ok);
+      if ((threadIdx.x & 63) == 0) set_error(ts, 2, b * 64 + (__ffsll((long long)miss) - 1), ndep);
       return true;
     }
     __builtin_amdgcn_s_sleep(32);
@@ -1731,6 +1775,7 @@ static void enqueue_phase_c(const Scene& sc, const Cam& cam, bool st, int W, int
 }
 
 size_t team_state_bytes() { return sizeof(TeamState); }
+size_t team_dq_offset() { return offsetof(TeamState, dq); }
 
 // k_side workgroups per CU such that one resolver workgroup (one wave per SIMD) still fits
 // beside them in every SIMD's 512 VGPRs: k_side waits for the resolver's census, so it must

@@ -178,3 +178,31 @@ def random_scene(rng, path, n_shapes, n_lights):
                      f"{pos[1]:.2f}, {pos[2]:.2f}]{extra}")
     with open(path, "w") as f:
         f.write("\n".join(lines) + "\n")
+
+
+QUADRIC_POINT_LIGHT = ("light, color: [4, 4, 4], radial-a2: 0.01, radial-a1: 0.0125, "
+                       "radial-a0: 0.0125, position: [10, 10, -5]")
+# Scenes whose phantom record (shapes_list[-1], C/raycast.c:382) is LIT: the reference's output
+# depends on the light-VLA bytes it aliases, deterministically.
+#   four-lights: phantom = light bytes [184, 288): L2's cos_theta/a0/direction/type and
+#                reflectivity/refractivity = L3.pos[1], L3.pos[2]
+#   two-lights:  phantom = light bytes [40, 144): L0's cos_theta/a0/direction/type and
+#                reflectivity/refractivity = L1.pos[1], L1.pos[2] (here 0.25 + 0.125 < 1)
+PHANTOM_LIT = {
+    "four-lights": QUADRIC_POINT_LIGHT + "\n"
+    "light, color: [1, 1, 1], radial-a2: 0.05, radial-a1: 0.1, radial-a0: 0.1, "
+    "position: [-3, 4, 2], theta: 0.3, angular-a0: 1, direction: [0.3, 0.2, 0.9]\n"
+    "light, color: [0.5, 0.5, 0.5], radial-a2: 0.05, radial-a1: 0.1, radial-a0: 0.1, "
+    "position: [2, 0.25, 0.125]",
+    "two-lights": "light, color: [4, 4, 4], radial-a2: 0.01, radial-a1: 0.0125, "
+    "radial-a0: 0.0125, position: [10, 0.25, 0.125]",
+}
+
+
+def phantom_lit_scene(path, kind):
+    """quadric.scene with its point light replaced so that the phantom is lit (PHANTOM_LIT)."""
+    text = open(scene_path("quadric")).read().rstrip("\n")
+    assert QUADRIC_POINT_LIGHT in text
+    with open(path, "w") as f:
+        f.write(text.replace(QUADRIC_POINT_LIGHT, PHANTOM_LIT[kind]) + "\n")
+    return path

@@ -297,3 +297,63 @@ def test_degenerate_scenes(case, tmp_path):
     rc.frames_wait()
     for buf, want, msg in bufs:
         np.testing.assert_array_equal(buf.cpu().numpy(), want, err_msg=msg)
+
+
+PHANTOM_TABLE = os.path.join(GOLDEN, "phantom_md5.json")
+
+
+def test_phantom_lit():
+    """Scenes whose phantom record is lit (shapes_list[-1], C/raycast.c:87-89,382; SURVEY.md §8
+    a15): four lights (light bytes [184, 288)) and two lights with L1.pos.y + L1.pos.z < 1
+    (bytes [40, 144)).  Every reflection miss shades the phantom, so the device's phantom
+    record and phase C without the clean-entry shortcut (Scene::dep_fast = 0) decide the
+    bytes.  Parity: md5 of the reference's own output (tests/golden/make_phantom_golden.py) at
+    depths 1/4/6, one frame at a time and with frames in flight; fast mode against the oracle."""
+    import json
+    torch = pytest.importorskip("torch")
+    table = json.load(open(PHANTOM_TABLE))
+    scenes = {n: rc.Scene.from_file(scene_path(n)) for n in ("phantom_four", "phantom_two")}
+    jobs = []
+    for key, want in sorted(table.items()):
+        name, size, d, mode = key.split(":")
+        w, h = map(int, size.split("x"))
+        img = rc.render(scenes[name], w, h, depth=int(d[1:]), mode=mode)
+        assert p3_md5(img) == want["md5"], key
+        jobs.append((key, name, w, h, int(d[1:]),
+                     torch.empty((h, w, 3), dtype=torch.uint8, device="cuda")))
+    torch.cuda.synchronize()
+    for key, name, w, h, d, buf in jobs:
+        rc.frame_submit(scenes[name], w, h, buf.data_ptr(), depth=d, mode="parity")
+    rc.frames_wait()
+    for key, name, w, h, d, buf in jobs:
+        assert p3_md5(buf.cpu().numpy()) == table[key]["md5"], key + " in flight"
+    for name, s in scenes.items():
+        for d in (1, 4, 6):
+            want, st = oracle_render(s, 200, 150, d, "fast")
+            np.testing.assert_array_equal(rc.render(s, 200, 150, depth=d, mode="fast"), want,
+                                          err_msg=f"{name} fast d{d}")
+
+
+def test_bench_sequence_8192(table):
+    """bench.py's order at the C5 image size (a lone frame issued after the frame
+    pipeline once timed out): lone rc_render_device frames, then >= 20 frames in flight, then
+    lone rc_render frames into host memory — every image md5-equal to the reference's."""
+    torch = pytest.importorskip("torch")
+    n = 8192
+    want = table["quadric:8192x8192:d6:parity"]["md5"]
+    s = rc.Scene.from_file(scene_path("quadric"))
+    out = torch.empty((n, n, 3), dtype=torch.uint8, device="cuda")
+    for _ in range(2):
+        rc.render_device(s, n, n, out.data_ptr(), depth=6, mode="parity")
+    torch.cuda.synchronize()
+    assert p3_md5(out.cpu().numpy()) == want, "lone device frame"
+    outs = [torch.empty((n, n, 3), dtype=torch.uint8, device="cuda") for _ in range(4)]
+    torch.cuda.synchronize()
+    for i in range(22):
+        rc.frame_submit(s, n, n, outs[i % 4].data_ptr(), depth=6, mode="parity")
+    rc.frames_wait()
+    for o in outs:
+        assert p3_md5(o.cpu().numpy()) == want, "in flight"
+    del outs
+    for i in range(2):
+        assert p3_md5(rc.render(s, n, n, depth=6, mode="parity")) == want, f"lone rc_render {i}"

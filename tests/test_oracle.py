@@ -5,12 +5,13 @@ writes (C/ sources built exactly as C/Makefile:4, tests/golden/make_golden.py), 
 small.npz the decoded 64x64 images.  When oracle/_ref is present the oracle is also
 compared image-for-image with the reference on seeded random scenes.
 """
+import json
 import os
 
 import numpy as np
 import pytest
 
-from helpers import (GOLDEN, SCENES, golden_key, golden_table, have_ref, oracle_render, p3_md5,
+from helpers import (GOLDEN, PHANTOM_LIT, SCENES, golden_key, golden_table, have_ref, oracle_render, p3_md5, phantom_lit_scene,
                      rc, run_ref, scene_path, random_scene)
 
 SMALL = ["simple", "reflection", "quadric", "example2", "example3", "quadric2"]
@@ -99,22 +100,29 @@ def test_oracle_vs_reference_many_shapes(n_shapes, tmp_path):
 
 
 @pytest.mark.skipif(not have_ref(), reason="oracle/_ref not built (make ref)")
-def test_phantom_model_four_lights(tmp_path):
-    """shapes_list[-1] with 4 lights = light-VLA bytes [184, 288): diffuse/specular from
-    L2 (cos_theta, a0, direction, type) and reflectivity/refractivity = L3.pos[1], pos[2].
-    Chosen so the phantom is lit (opacity > 0): the image depends on the model."""
-    path = str(tmp_path / "ph4.scene")
-    with open(path, "w") as f:
-        f.write(open(scene_path("quadric")).read().rstrip("\n").replace(
-            "light, color: [4, 4, 4], radial-a2: 0.01, radial-a1: 0.0125, radial-a0: 0.0125, "
-            "position: [10, 10, -5]",
-            "light, color: [4, 4, 4], radial-a2: 0.01, radial-a1: 0.0125, radial-a0: 0.0125, "
-            "position: [10, 10, -5]\n"
-            "light, color: [1, 1, 1], radial-a2: 0.05, radial-a1: 0.1, radial-a0: 0.1, "
-            "position: [-3, 4, 2], theta: 0.3, angular-a0: 1, direction: [0.3, 0.2, 0.9]\n"
-            "light, color: [0.5, 0.5, 0.5], radial-a2: 0.05, radial-a1: 0.1, radial-a0: 0.1, "
-            "position: [2, 0.25, 0.125]") + "\n")
+@pytest.mark.parametrize("kind", sorted(PHANTOM_LIT))
+def test_phantom_model_lit(kind, tmp_path):
+    """A lit phantom (opacity > 0) makes the image depend on the light-VLA bytes the
+    reference reads as shapes_list[-1]: four lights (bytes [184, 288)) and two lights with
+    L1.pos.y + L1.pos.z < 1 (bytes [40, 144)).  Oracle == the reference binary."""
+    path = phantom_lit_scene(str(tmp_path / f"{kind}.scene"), kind)
     s = rc.Scene.from_file(path)
-    img, st = oracle_render(s, 96, 96, 6, "parity")
-    assert st["parity_defined"] == 1 and st["phantom_shades"] > 0
-    np.testing.assert_array_equal(img, run_ref(path, 96, 96, 6, "parity"))
+    for d in (1, 4, 6):
+        img, st = oracle_render(s, 96, 96, d, "parity")
+        assert st["parity_defined"] == 1 and st["phantom_shades"] > 0, (kind, d)
+        np.testing.assert_array_equal(img, run_ref(path, 96, 96, d, "parity"), err_msg=f"{kind} d{d}")
+
+
+def test_phantom_goldens():
+    """The oracle reproduces the reference's lit-phantom images (tests/golden/phantom_md5.json,
+    made by tests/golden/make_phantom_golden.py from the reference build)."""
+    table = json.load(open(os.path.join(GOLDEN, "phantom_md5.json")))
+    scenes = {}
+    for key, want in sorted(table.items()):
+        name, size, d, mode = key.split(":")
+        w, h = map(int, size.split("x"))
+        if name not in scenes:
+            scenes[name] = rc.Scene.from_file(os.path.join(SCENES, name + ".scene"))
+        img, st = oracle_render(scenes[name], w, h, int(d[1:]), mode)
+        assert st["phantom_shades"] > 0, key
+        assert p3_md5(img) == want["md5"], key
