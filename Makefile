@@ -71,3 +71,13 @@ ref:
 clean:
 	rm -rf $(LIB) $(BIN)
 	$(MAKE) -C oracle clean
+
+# measurement variants of the pixel kernels' framebuffer store (RC_HIP_LIB=libraycast_hip_<v>.so):
+#   coalesced: 32x8 tiles staged in LDS, whole-row stores; t16: 16x16 tiles staged in LDS
+variants: $(LIB)/libraycast_hip_coalesced.so $(LIB)/libraycast_hip_t16.so
+$(OBJ)/coalesced_kernels.o: $(SRC)/rc_kernels.hip $(HIP_HDRS)
+	$(HIPCC) $(HIPFLAGS) -DRC_TILE_W=32 -DRC_TILE_STAGE=1 -c $< -o $@
+$(OBJ)/t16_kernels.o: $(SRC)/rc_kernels.hip $(HIP_HDRS)
+	$(HIPCC) $(HIPFLAGS) -DRC_TILE_W=16 -DRC_TILE_STAGE=1 -c $< -o $@
+$(LIB)/libraycast_hip_%.so: $(OBJ)/%_kernels.o $(OBJ)/rc_api.o $(OBJ)/rc_scene.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -o $@ -lpthread

@@ -218,10 +218,13 @@ def options(depth=6, mode="parity", gpus=1, device=0):
     return opt
 
 
-def render(scene, width, height, depth=6, mode="parity", gpus=1, device=0, timing=None):
-    """Render to a host array [H, W, 3] uint8 through rc_render (the raycast() path)."""
+def render(scene, width, height, depth=6, mode="parity", gpus=1, device=0, timing=None, out=None):
+    """Render to a host array [H, W, 3] uint8 through rc_render (the raycast() path); `out`
+    (optional) is the caller's C-contiguous pixmap, like the reference's malloc'd one."""
     lib = hip_lib()
-    out = np.empty((height, width, 3), dtype=np.uint8)
+    if out is None:
+        out = np.empty((height, width, 3), dtype=np.uint8)
+    assert out.shape == (height, width, 3) and out.dtype == np.uint8 and out.flags.c_contiguous
     t = RcTiming()
     opt = options(depth, mode, gpus, device)
     rc = lib.rc_render(scene.packed(), width, height, ctypes.byref(opt),

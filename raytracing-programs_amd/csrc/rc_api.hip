@@ -19,6 +19,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -134,6 +135,17 @@ struct DevCtx {
   int res_blocks[kResCache] = {};
   size_t parity_pixels = 0;
   int parity_rows = 0;
+  // rc_render's overlapped copy (parity): the framebuffer leaves on `d2h` while the resolver
+  // runs, then only the DEP entries' colours (`patch`, packed RGB per entry) follow
+  hipStream_t d2h = nullptr;
+  DevBuf patch;
+  uint8_t* pin_pix = nullptr;     // pinned: DEP pixel indices (int64 per entry)
+  uint8_t* pin_patch = nullptr;   // pinned: DEP entries' packed RGB
+  size_t pin_bytes = 0;           // capacity of each pinned buffer, in entries
+  int* pin_cnt = nullptr;         // pinned: counters[0..3]
+  // One render at a time per device: the workspace, TeamState, events and streams above are
+  // shared by every call on this device (rc_render, rc_render_device, rc_frame_submit).
+  std::mutex mu;
 };
 
 DevCtx g_ctx[kMaxDevices];
@@ -168,60 +180,57 @@ int ctx_get(int device, DevCtx** out) {
 // threads) and copies each chunk out with a small persistent thread pool.
 constexpr size_t kStageChunk = 8u << 20;
 
-class CopyPool {
+class HostPool {
  public:
-  static CopyPool& get() {   // never destroyed: its detached workers outlive main()
-    static CopyPool* pool = new CopyPool();
+  static HostPool& get() {   // never destroyed: its detached workers outlive main()
+    static HostPool* pool = new HostPool();
     return *pool;
   }
-  // memcpy(dst, src, n) split over the workers and the calling thread
-  void copy(uint8_t* dst, const uint8_t* src, size_t n) {
-    std::lock_guard<std::mutex> one_at_a_time(call_mu_);   // concurrent rc_render callers
-    const int parts = nthreads_ + 1;
-    const size_t step = ((n + parts - 1) / parts + 4095) & ~(size_t)4095;
+  int parts() const { return nthreads_ + 1; }
+  // fn(part, parts) on the workers and the calling thread (part 0), one call at a time
+  void run(const std::function<void(int, int)>& fn) {
+    std::lock_guard<std::mutex> one_at_a_time(call_mu_);   // rc_render callers on other devices
     {
       std::unique_lock<std::mutex> lk(mu_);
-      dst_ = dst;
-      src_ = src;
-      n_ = n;
-      step_ = step;
+      fn_ = &fn;
       pending_ = nthreads_;
       ++gen_;
     }
     cv_.notify_all();
-    const size_t len = n < step ? n : step;   // part 0
-    std::memcpy(dst, src, len);
+    fn(0, nthreads_ + 1);
     std::unique_lock<std::mutex> lk(mu_);
     done_.wait(lk, [&] { return pending_ == 0; });
   }
+  // memcpy(dst, src, n) split over the pool
+  void copy(uint8_t* dst, const uint8_t* src, size_t n) {
+    const size_t step = ((n + parts() - 1) / parts() + 4095) & ~(size_t)4095;
+    run([&](int part, int) {
+      const size_t off = (size_t)part * step;
+      if (off < n) std::memcpy(dst + off, src + off, n - off < step ? n - off : step);
+    });
+  }
 
  private:
-  CopyPool() {
+  HostPool() {
     int t = 7;
     if (const char* e = std::getenv("RC_COPY_THREADS")) t = std::atoi(e) - 1;
     if (t < 0) t = 0;
     if (t > 31) t = 31;
     nthreads_ = t;
-    for (int i = 0; i < t; ++i) workers_.emplace_back([this, i] { run(i + 1); });
+    for (int i = 0; i < t; ++i) workers_.emplace_back([this, i] { work(i + 1); });
     for (auto& w : workers_) w.detach();   // lives for the process
   }
-  void run(int part) {
+  void work(int part) {
     unsigned long long seen = 0;
     for (;;) {
-      uint8_t* dst;
-      const uint8_t* src;
-      size_t n, step;
+      const std::function<void(int, int)>* fn;
       {
         std::unique_lock<std::mutex> lk(mu_);
         cv_.wait(lk, [&] { return gen_ != seen; });
         seen = gen_;
-        dst = dst_;
-        src = src_;
-        n = n_;
-        step = step_;
+        fn = fn_;
       }
-      const size_t off = (size_t)part * step;
-      if (off < n) std::memcpy(dst + off, src + off, n - off < step ? n - off : step);
+      (*fn)(part, nthreads_ + 1);
       std::unique_lock<std::mutex> lk(mu_);
       if (--pending_ == 0) done_.notify_one();
     }
@@ -232,9 +241,7 @@ class CopyPool {
   int nthreads_ = 0;
   unsigned long long gen_ = 0;
   int pending_ = 0;
-  uint8_t* dst_ = nullptr;
-  const uint8_t* src_ = nullptr;
-  size_t n_ = 0, step_ = 0;
+  const std::function<void(int, int)>* fn_ = nullptr;
 };
 
 int copy_to_host(DevCtx& c, uint8_t* host, const uint8_t* dev, size_t bytes, hipStream_t st) {
@@ -259,13 +266,79 @@ int copy_to_host(DevCtx& c, uint8_t* host, const uint8_t* dev, size_t bytes, hip
   for (size_t i = 0; i < n; ++i) {
     const int b = (int)(i & 1);
     HIP_TRY(hipEventSynchronize(c.stage_ev[b]));
-    CopyPool::get().copy(host + i * kStageChunk, c.stage[b], chunk(i));
+    HostPool::get().copy(host + i * kStageChunk, c.stage[b], chunk(i));
     if (i + 2 < n) {
       HIP_TRY(hipMemcpyAsync(c.stage[b], dev + (i + 2) * kStageChunk, chunk(i + 2),
                              hipMemcpyDeviceToHost, st));
       HIP_TRY(hipEventRecord(c.stage_ev[b], st));
     }
   }
+  return 0;
+}
+
+// Fault the caller's fresh pixmap in (C/raycast.c:52-53 mallocs it) over the host pool while the
+// GPU renders, instead of inside the copy (every byte is overwritten afterwards).
+void prefault(uint8_t* p, size_t n) {
+  if (!n || std::getenv("RC_NO_PREFAULT")) return;
+  HostPool::get().run([&](int part, int parts) {
+    const size_t per = ((n + parts - 1) / parts + 4095) & ~(size_t)4095;
+    const size_t a = (size_t)part * per, b = a + per < n ? a + per : n;
+    volatile uint8_t* q = p;
+    for (size_t o = a; o < b; o += 4096) q[o] = 0;
+    if (a < b) q[b - 1] = 0;
+  });
+}
+
+int ensure_pinned(DevCtx& c, size_t entries) {
+  if (!c.pin_cnt) HIP_TRY(hipHostMalloc((void**)&c.pin_cnt, 64, hipHostMallocDefault));
+  if (entries <= c.pin_bytes) return 0;
+  if (c.pin_pix) (void)hipHostFree(c.pin_pix);
+  if (c.pin_patch) (void)hipHostFree(c.pin_patch);
+  c.pin_pix = c.pin_patch = nullptr;
+  c.pin_bytes = 0;
+  HIP_TRY(hipHostMalloc((void**)&c.pin_pix, entries * sizeof(long long), hipHostMallocDefault));
+  HIP_TRY(hipHostMalloc((void**)&c.pin_patch, entries * sizeof(uint32_t), hipHostMallocDefault));
+  c.pin_bytes = entries;
+  return 0;
+}
+
+// The parity render's device-to-host copy, overlapped with the render (the
+// drop-in rate spans upload + kernels + copy).  Once phase A and the compaction are done
+// (ev[2]), every pixel except the DEP pixels is final: the framebuffer streams out on the copy
+// stream while the carry resolver runs, together with the DEP list (pixel per entry).  After
+// phase C (ev[4]) only the DEP entries' packed colours follow (4 B per entry, ~17 % of the
+// pixels), and the host pool scatters them over the copy.
+int copy_overlapped(DevCtx& c, uint8_t* host, const uint8_t* dev, size_t bytes,
+                    const hipEvent_t* ev) {
+  if (ensure_pinned(c, 0)) return -1;
+  HIP_TRY(hipEventSynchronize(ev[2]));
+  HIP_TRY(hipMemcpyAsync(c.pin_cnt, c.fb.counters.p, 4 * sizeof(int), hipMemcpyDeviceToHost,
+                         c.d2h));
+  HIP_TRY(hipStreamSynchronize(c.d2h));
+  const size_t ndep = (size_t)c.pin_cnt[2];
+  if (ensure_pinned(c, ndep)) return -1;
+  if (ndep)
+    HIP_TRY(hipMemcpyAsync(c.pin_pix, c.fb.dep_pix.p, ndep * sizeof(long long),
+                           hipMemcpyDeviceToHost, c.d2h));
+  if (copy_to_host(c, host, dev, bytes, c.d2h)) return -1;
+  HIP_TRY(hipEventSynchronize(ev[4]));
+  if (!ndep) return 0;
+  HIP_TRY(hipMemcpyAsync(c.pin_patch, c.patch.p, ndep * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                         c.d2h));
+  HIP_TRY(hipStreamSynchronize(c.d2h));
+  const long long* pix = (const long long*)c.pin_pix;
+  const uint32_t* rgb = (const uint32_t*)c.pin_patch;
+  HostPool::get().run([&](int part, int parts) {
+    const size_t per = (ndep + parts - 1) / parts;
+    const size_t a = (size_t)part * per, b = a + per < ndep ? a + per : ndep;
+    for (size_t j = a; j < b; ++j) {
+      uint8_t* q = host + 3 * (size_t)pix[j];
+      const uint32_t v = rgb[j];
+      q[0] = (uint8_t)v;
+      q[1] = (uint8_t)(v >> 8);
+      q[2] = (uint8_t)(v >> 16);
+    }
+  });
   return 0;
 }
 
@@ -488,7 +561,8 @@ int ensure_parity(DevCtx& c, FrameBufs& b, int W, int H, rc::ParityWork& w, int 
 
 // Enqueue one render of rows (row0 + k*row_step) into d_out on c.stream.
 int enqueue_render(DevCtx& c, const rc_scene* s, int W, int H, int row0, int row_step, int nrows,
-                   const rc_options* opt, uint8_t* d_out, hipStream_t stream, bool timed) {
+                   const rc_options* opt, uint8_t* d_out, hipStream_t stream, bool timed,
+                   uint32_t* patch = nullptr, hipEvent_t** evset = nullptr) {
   rc::LaunchScene ls;
   if (upload_scene(c.fb, stream, s, ls)) return -1;
   unsigned long long* zc = (unsigned long long*)c.fb.zcount.p;
@@ -501,6 +575,7 @@ int enqueue_render(DevCtx& c, const rc_scene* s, int W, int H, int row0, int row
     c.prof_calls++;
     c.prof_parity = parity;
   }
+  if (evset) *evset = ev;
   if (timed) HIP_TRY(hipEventRecord(ev[0], stream));
   if (!parity) {
     HIP_TRY(rc::launch_render(ls, W, H, row0, row_step, nrows, maxrec, d_out, zc, stream));
@@ -520,6 +595,7 @@ int enqueue_render(DevCtx& c, const rc_scene* s, int W, int H, int row0, int row
     return -1;
   }
   if (w.split_shade) ls.dep_fast = 0;   // k_classify leaves no primary shade
+  w.patch = patch;
   HIP_TRY(rc::launch_parity(ls, W, H, maxrec, d_out, w, zc, stream, timed ? ev + 1 : nullptr));
   return 0;
 }
@@ -686,6 +762,7 @@ int rc_render_device(const rc_scene* s, int W, int H, int row0, int row_step, in
   HIP_TRY(hipGetDevice(&dev));
   DevCtx* c;
   if (ctx_get(dev, &c)) return -1;
+  std::lock_guard<std::mutex> lk(c->mu);
   hipStream_t st = stream ? (hipStream_t)stream : c->stream;
   // the scene upload and events live on the ctx stream: order them with the caller's stream
   if (st != c->stream) {
@@ -813,6 +890,7 @@ int rc_frame_submit(const rc_scene* s, int W, int H, const rc_options* opt, uint
   HIP_TRY(hipGetDevice(&dev));
   DevCtx* c;
   if (ctx_get(dev, &c)) return -1;
+  std::lock_guard<std::mutex> lk(c->mu);
   const int maxrec = opt->max_recursion;
   if (!(opt->mode == RC_MODE_PARITY && maxrec > 1)) {   // no serial stage: whole GPU, in order
     if (enqueue_render(*c, s, W, H, 0, 1, H, opt, d_out, c->stream, false)) return -1;
@@ -868,6 +946,7 @@ int rc_frames_wait(rc_timing* timing) {
   HIP_TRY(hipGetDevice(&dev));
   DevCtx* c;
   if (ctx_get(dev, &c)) return -1;
+  std::lock_guard<std::mutex> lk(c->mu);
   Pipe& p = c->pipe;
   if (timing) std::memset(timing, 0, sizeof *timing);
   HIP_TRY(hipStreamSynchronize(c->stream));
@@ -910,6 +989,7 @@ int rc_pipe_reset(void) {
   DevCtx* c;
   if (ctx_get(dev, &c)) return -1;
   const int rc = rc_frames_wait(nullptr);
+  std::lock_guard<std::mutex> lk(c->mu);
   pipe_release(*c);
   return rc;
 }
@@ -992,20 +1072,40 @@ int rc_render(const rc_scene* s, int W, int H, const rc_options* opt, uint8_t* p
       return;
     }
     uint8_t* d_out = (uint8_t*)c->out.p;
-    if (enqueue_render(*c, s, W, H, g, G, nrows, opt, d_out, c->stream, true)) {
+    std::lock_guard<std::mutex> lk(c->mu);
+    // parity, one device: the copy overlaps the resolver (copy_overlapped); split shading
+    // leaves the non-DEP colours to phase C, so its framebuffer is not final after phase A
+    const bool overlap = G == 1 && parity && !std::getenv("RC_SPLIT_SHADE") &&
+                         !std::getenv("RC_SERIAL_D2H");
+    uint32_t* patch = nullptr;
+    if (overlap) {
+      if ((!c->d2h && hipStreamCreateWithFlags(&c->d2h, hipStreamNonBlocking) != hipSuccess) ||
+          c->patch.ensure((size_t)W * H * sizeof(uint32_t))) {
+        rcodes[g] = -1;
+        return;
+      }
+      patch = (uint32_t*)c->patch.p;
+    }
+    hipEvent_t* ev = nullptr;
+    if (enqueue_render(*c, s, W, H, g, G, nrows, opt, d_out, c->stream, true, patch, &ev)) {
       rcodes[g] = -1;
       return;
     }
-    // The caller's pixmap is typically fresh from malloc (C/raycast.c:52-53): fault its pages
-    // in while the GPU renders, instead of inside the copy (every byte is overwritten).
-    if (!std::getenv("RC_NO_PREFAULT")) {
+    if (G == 1) {
+      prefault(pixmap, (size_t)H * row_bytes);
+    } else if (!std::getenv("RC_NO_PREFAULT")) {
       volatile uint8_t* p = pixmap + (size_t)g * row_bytes;
-      const size_t span = G == 1 ? (size_t)H * row_bytes : ((size_t)(nrows - 1) * G + 1) * row_bytes;
+      const size_t span = ((size_t)(nrows - 1) * G + 1) * row_bytes;
       for (size_t o = 0; o < span; o += 4096) p[o] = 0;
       if (span) p[span - 1] = 0;
     }
     auto td = std::chrono::steady_clock::now();
-    if (G == 1) {   // contiguous image: staged, multi-threaded copy
+    if (overlap) {
+      if (copy_overlapped(*c, pixmap, d_out, (size_t)H * row_bytes, ev)) {
+        rcodes[g] = -1;
+        return;
+      }
+    } else if (G == 1) {   // contiguous image: staged, multi-threaded copy
       if (copy_to_host(*c, pixmap, d_out, (size_t)H * row_bytes, c->stream)) {
         rcodes[g] = -1;
         return;

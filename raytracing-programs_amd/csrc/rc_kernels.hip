@@ -31,19 +31,110 @@
 
 namespace rc {
 
-constexpr int kTile = 16;        // 16x16 pixels per workgroup, 256 lanes
-constexpr int kBlock = kTile * kTile;
+// Pixel kernels: a workgroup renders a 16x16-pixel tile of four 8x8 wave tiles (ray coherence
+// inside a wave); each lane stores its own three framebuffer bytes.  The LDS-staged form
+// (RC_TILE_STAGE=1, built as libraycast_hip_coalesced.so with 32x8 tiles) writes every tile row
+// as one 96-byte run instead: rocprofv3 WRITE_SIZE of k_render at quadric 4096^2 50.6 MB (=
+// the 50.3 MB framebuffer) against 64.0 MB for the lane stores, but k_render 0.74-0.76 ms
+// against 0.69 ms and phase A 0.93-0.96 against 0.86 ms: these kernels are VALU-
+// bound and their stores use < 1 % of HBM bandwidth, so the lane stores are the default.
+#ifndef RC_TILE_W
+#define RC_TILE_W 16
+#endif
+#ifndef RC_TILE_STAGE
+#define RC_TILE_STAGE 0   // 1: tiles staged in LDS, written as whole rows (variant)
+#endif
+constexpr int kTileW = RC_TILE_W, kTileH = 256 / RC_TILE_W;
+constexpr int kBlock = kTileW * kTileH;
+static_assert(kTileW % 8 == 0 && kTileH % 8 == 0, "8x8 wave tiles");
 
 __device__ __forceinline__ void tile_pixel(int& lx, int& ly) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  lx = (wave & 1) * 8 + (lane & 7);
-  ly = (wave >> 1) * 8 + (lane >> 3);
+  lx = (wave % (kTileW / 8)) * 8 + (lane & 7);
+  ly = (wave / (kTileW / 8)) * 8 + (lane >> 3);
+}
+
+// A tile's framebuffer bytes (and, for phase A, its class bytes) staged in LDS: every lane
+// drops its 3 (1) bytes in, then the workgroup writes each row of the tile as one contiguous
+// run — dword stores when the run is whole and 4-byte aligned (W % 4 == 0), bytes otherwise —
+// instead of three byte stores per lane into 8-pixel row fragments (the store
+// north_star names is the coalesced one; C/raycast.c:122-127 is the store replaced).
+struct TileBytes {
+  uint32_t rgb[kTileH][kTileW * 3 / 4];
+  uint32_t cls[kTileH][kTileW / 4];
+  int done;   // waves that have staged their pixels
+};
+
+// Zeroes the wave counter; the caller's next barrier publishes it.
+__device__ __forceinline__ void tile_init(TileBytes& t) {
+  if (threadIdx.x == 0) t.done = 0;
+}
+
+// No workgroup barrier before the row writes (waiting for the slowest wave of a tile held the
+// others' slots: measured +7 % on k_render): each wave releases its staged bytes and counts
+// itself in; the LAST wave of the tile writes every row and the others simply end.
+__device__ __forceinline__ bool tile_last_wave(TileBytes& t) {
+  if (!RC_TILE_STAGE) return false;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  int old = 0;
+  if ((threadIdx.x & 63) == 0)
+    old = __hip_atomic_fetch_add(&t.done, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+  old = __shfl(old, 0, 64);
+  if (old != kBlock / 64 - 1) return false;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  return true;
+}
+
+__device__ __forceinline__ void tile_put_rgb(TileBytes& t, int lx, int ly, uint8_t r, uint8_t g,
+                                             uint8_t b, uint8_t* direct) {
+  if (!RC_TILE_STAGE) {   // the default: the lane's own three byte stores
+    direct[0] = r;
+    direct[1] = g;
+    direct[2] = b;
+    return;
+  }
+  uint8_t* q = (uint8_t*)t.rgb[ly] + lx * 3;
+  q[0] = r;
+  q[1] = g;
+  q[2] = b;
+}
+
+// Row ly of the tile goes to dst_row(ly) (nullptr: the row is outside the image), nbytes
+// valid bytes per row.  The tile's last wave calls this (tile_last_wave).
+template <int kWords, typename RowPtr>
+__device__ __forceinline__ void tile_write_rows(const uint32_t (*src)[kWords], RowPtr dst_row,
+                                                int nbytes) {
+  const int t = threadIdx.x & 63;   // one wave writes the tile (tile_last_wave)
+  for (int i = t; i < kTileH * kWords; i += 64) {
+    const int ly = i / kWords, k = i % kWords;
+    uint8_t* d = dst_row(ly);
+    if (!d) continue;
+    if (nbytes == kWords * 4 && ((uintptr_t)d & 3u) == 0u) {
+      ((uint32_t*)d)[k] = src[ly][k];
+    } else {
+      const uint8_t* sb = (const uint8_t*)src[ly];
+      for (int b = k * 4; b < k * 4 + 4 && b < nbytes; ++b) d[b] = sb[b];
+    }
+  }
 }
 
 __device__ __forceinline__ void store_rgb(uint8_t* __restrict__ p, V3 c) {
   p[0] = quant(c.x);
   p[1] = quant(c.y);
   p[2] = quant(c.z);
+}
+
+// Phase C's store of DEP entry j at pixel p: the framebuffer, and — when the host is copying
+// the framebuffer out while the resolver runs (rc_render) — the entry's packed RGB in `patch`,
+// which the host then scatters over the DEP pixels of its copy.
+__device__ __forceinline__ void store_dep(uint8_t* __restrict__ out, uint32_t* __restrict__ patch,
+                                          long long p, int j, V3 c) {
+  const uint8_t r = quant(c.x), g = quant(c.y), b = quant(c.z);
+  uint8_t* q = out + (size_t)p * 3;
+  q[0] = r;
+  q[1] = g;
+  q[2] = b;
+  if (patch) patch[j] = (uint32_t)r | ((uint32_t)g << 8) | ((uint32_t)b << 16);
 }
 
 __device__ __forceinline__ void flush_events(int zero_events, unsigned long long* counter) {
@@ -92,19 +183,30 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_
                                                    uint8_t* __restrict__ out,
                                                    unsigned long long* __restrict__ zcount) {
   __shared__ StageBuf<kStage> stage;
+  __shared__ TileBytes tb;
+  tile_init(tb);
   stage_scene<kStage>(sc, stage);
+  if (!kStage) __syncthreads();
   int lx, ly;
   tile_pixel(lx, ly);
-  const int x = blockIdx.x * kTile + lx;
-  const int r = blockIdx.y * kTile + ly;           // local (shard) row
-  if (x >= W || r >= nrows) return;
-  const int y = row0 + r * row_step;
-  int zero = 0;
-  const V3 d = primary_dir(cam, x, y, zero);
-  PixelOut po;
-  shoot<kModeFast>(sc, d, maxrec, v3(0.0f, 0.0f, 0.0f), po, zero);
-  store_rgb(out + ((size_t)r * W + x) * 3, po.rgb);
-  flush_events(zero, zcount);
+  const int x0 = blockIdx.x * kTileW, r0 = blockIdx.y * kTileH;
+  const int x = x0 + lx;
+  const int r = r0 + ly;           // local (shard) row
+  if (x < W && r < nrows) {
+    const int y = row0 + r * row_step;
+    int zero = 0;
+    const V3 d = primary_dir(cam, x, y, zero);
+    PixelOut po;
+    shoot<kModeFast>(sc, d, maxrec, v3(0.0f, 0.0f, 0.0f), po, zero);
+    tile_put_rgb(tb, lx, ly, quant(po.rgb.x), quant(po.rgb.y), quant(po.rgb.z),
+                 out + ((size_t)r * W + x) * 3);
+    flush_events(zero, zcount);
+  }
+  if (!tile_last_wave(tb)) return;
+  const int nx = W - x0 < kTileW ? W - x0 : kTileW;
+  tile_write_rows<kTileW * 3 / 4>(tb.rgb, [&](int q) -> uint8_t* {
+    return r0 + q < nrows ? out + ((size_t)(r0 + q) * W + x0) * 3 : nullptr;
+  }, nx * 3);
 }
 
 // ------------------------------------------------------------------ parity phase A --
@@ -116,29 +218,46 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_
                                                     DepRec* __restrict__ deprec,
                                                     unsigned long long* __restrict__ zcount) {
   __shared__ StageBuf<kStage> stage;
+  __shared__ TileBytes tb;
+  tile_init(tb);
   stage_scene<kStage>(sc, stage);
+  if (!kStage) __syncthreads();
   int lx, ly;
   tile_pixel(lx, ly);
-  const int x = blockIdx.x * kTile + lx;
-  const int y = blockIdx.y * kTile + ly;
-  if (x >= W || y >= H) return;
-  const size_t p = (size_t)y * W + x;
-  int zero = 0;
-  const V3 d = primary_dir(cam, x, y, zero);
-  PixelOut po;
-  shoot<kModeParityA>(sc, d, maxrec, v3(0.0f, 0.0f, 0.0f), po, zero);
-  cls[p] = po.cls;
-  if (po.cls == kClsDep) {
-    deprec[p] = po.dep;
-    if (sc.dep_fast) {      // primary shade for phase C; this part's events are counted here
-      wcarry[p] = make_float4(po.pcol.x, po.pcol.y, po.pcol.z, 0.0f);
+  const int x0 = blockIdx.x * kTileW, y0 = blockIdx.y * kTileH;
+  const int x = x0 + lx;
+  const int y = y0 + ly;
+  if (x < W && y < H) {
+    const size_t p = (size_t)y * W + x;
+    int zero = 0;
+    const V3 d = primary_dir(cam, x, y, zero);
+    PixelOut po;
+    shoot<kModeParityA>(sc, d, maxrec, v3(0.0f, 0.0f, 0.0f), po, zero);
+    if (RC_TILE_STAGE) ((uint8_t*)tb.cls[ly])[lx] = po.cls;
+    else cls[p] = po.cls;
+    if (po.cls == kClsDep) {
+      deprec[p] = po.dep;
+      // primary shade for phase C; this part's events are counted here (else phase C
+      // recomputes the whole pixel and counts its events).  The pixel's framebuffer bytes
+      // are phase C's: the tile writes a placeholder there.
+      if (sc.dep_fast) {
+        wcarry[p] = make_float4(po.pcol.x, po.pcol.y, po.pcol.z, 0.0f);
+        flush_events(zero, zcount);
+      }
+      if (RC_TILE_STAGE) tile_put_rgb(tb, lx, ly, 0, 0, 0, nullptr);
+    } else {
+      if (po.cls == kClsWriter) wcarry[p] = make_float4(po.carry.x, po.carry.y, po.carry.z, 0.0f);
+      tile_put_rgb(tb, lx, ly, quant(po.rgb.x), quant(po.rgb.y), quant(po.rgb.z), out + p * 3);
       flush_events(zero, zcount);
-    }                       // else phase C recomputes the whole pixel (and counts its events)
-    return;
+    }
   }
-  if (po.cls == kClsWriter) wcarry[p] = make_float4(po.carry.x, po.carry.y, po.carry.z, 0.0f);
-  store_rgb(out + p * 3, po.rgb);
-  flush_events(zero, zcount);
+  if (!tile_last_wave(tb)) return;
+  const int nx = W - x0 < kTileW ? W - x0 : kTileW;
+  auto row_at = [&](uint8_t* base, int q, int bpp) -> uint8_t* {
+    return y0 + q < H ? base + ((size_t)(y0 + q) * W + x0) * bpp : nullptr;
+  };
+  tile_write_rows<kTileW * 3 / 4>(tb.rgb, [&](int q) { return row_at(out, q, 3); }, nx * 3);
+  tile_write_rows<kTileW / 4>(tb.cls, [&](int q) { return row_at(cls, q, 1); }, nx);
 }
 
 // Phase A's carry part only (no shading): k_side shades the non-DEP pixels off the critical path.
@@ -151,8 +270,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_
   stage_scene<kStage>(sc, stage);
   int lx, ly;
   tile_pixel(lx, ly);
-  const int x = blockIdx.x * kTile + lx;
-  const int y = blockIdx.y * kTile + ly;
+  const int x = blockIdx.x * kTileW + lx;
+  const int y = blockIdx.y * kTileH + ly;
   if (x >= W || y >= H) return;
   const size_t p = (size_t)y * W + x;
   int zero = 0;   // events are counted by the shading passes
@@ -1412,21 +1531,21 @@ __device__ __forceinline__ void shade_batch(const Scene& sc, const Cam& cam, int
                                             const DepRec* __restrict__ deprec,
                                             const float4* __restrict__ pcol, int ndep, int b,
                                             V3 c, bool hit, uint8_t* __restrict__ out,
-                                            int& zero) {
+                                            uint32_t* __restrict__ patch, int& zero) {
   const int j = b * 64 + (int)(threadIdx.x & 63);
   if (j >= ndep) return;
   const long long p = dep_pix[j];
   if (sc.dep_fast) {
     const float4 k = pcol[p];
     const V3 pc = v3(k.x, k.y, k.z);
-    store_rgb(out + (size_t)p * 3, hit ? shade_dep_cont(sc, deprec[p], maxrec, c, pc, zero) : pc);
+    store_dep(out, patch, p, j, hit ? shade_dep_cont(sc, deprec[p], maxrec, c, pc, zero) : pc);
     return;
   }
   const int y = (int)(p / W), x = (int)(p % W);
   const V3 d = primary_dir(cam, x, y, zero);
   PixelOut po;
   shoot<kModeParityC>(sc, d, maxrec, c, po, zero);
-  store_rgb(out + (size_t)p * 3, po.rgb);
+  store_dep(out, patch, p, j, po.rgb);
 }
 
 __device__ __forceinline__ int wave_ticket(int* ctr) {
@@ -1458,7 +1577,8 @@ __device__ __forceinline__ void phase_c_passes(const Scene& sc, const Cam& cam, 
                                                const float4* __restrict__ pcol,
                                                CinG* __restrict__ cin, int* __restrict__ counters,
                                                int* __restrict__ batch_state,
-                                               uint8_t* __restrict__ out, TeamState* ts,
+                                               uint8_t* __restrict__ out,
+                                               uint32_t* __restrict__ patch, TeamState* ts,
                                                unsigned tag, bool pass1, int& zero) {
   int* done_ctr = &counters[pass1 ? 9 : 11];
   const int ndep = counters[2];
@@ -1472,7 +1592,7 @@ __device__ __forceinline__ void phase_c_passes(const Scene& sc, const Cam& cam, 
     int mine = 0;
     if ((threadIdx.x & 63) == 0) mine = batch_claim(batch_state, b);
     if (!__shfl(mine, 0, 64)) continue;
-    shade_batch(sc, cam, W, maxrec, dep_pix, deprec, pcol, ndep, b, c, hit, out, zero);
+    shade_batch(sc, cam, W, maxrec, dep_pix, deprec, pcol, ndep, b, c, hit, out, patch, zero);
     if ((threadIdx.x & 63) == 0) atomicAdd(done_ctr, 1);
   }
   for (;;) {
@@ -1484,7 +1604,7 @@ __device__ __forceinline__ void phase_c_passes(const Scene& sc, const Cam& cam, 
     V3 c = v3(0.0f, 0.0f, 0.0f);
     bool hit = true;
     (void)batch_carries(cin, ndep, b, tag, true, c, hit, ts);
-    shade_batch(sc, cam, W, maxrec, dep_pix, deprec, pcol, ndep, b, c, hit, out, zero);
+    shade_batch(sc, cam, W, maxrec, dep_pix, deprec, pcol, ndep, b, c, hit, out, patch, zero);
     if ((threadIdx.x & 63) == 0) atomicAdd(done_ctr, 1);
   }
 }
@@ -1494,7 +1614,7 @@ __global__ void __launch_bounds__(kSideBlock) k_side(
     Scene sc, Cam cam, int W, int H, int maxrec, const uint8_t* __restrict__ cls,
     const long long* __restrict__ dep_pix, const DepRec* __restrict__ deprec,
     const float4* __restrict__ pcol, CinG* __restrict__ cin, int* __restrict__ counters,
-    int* __restrict__ batch_state, uint8_t* __restrict__ out,
+    int* __restrict__ batch_state, uint8_t* __restrict__ out, uint32_t* __restrict__ patch,
     unsigned long long* __restrict__ zcount, TeamState* __restrict__ ts, int resolve_blocks,
     unsigned tag, int tiles) {
   __shared__ int s_go;
@@ -1528,7 +1648,7 @@ __global__ void __launch_bounds__(kSideBlock) k_side(
     shade_tile(sc, cam, W, H, maxrec, t, cls, out, zero);
     if ((threadIdx.x & 63) == 0) atomicAdd(&counters[8], 1);
   }
-  phase_c_passes(sc, cam, W, maxrec, dep_pix, deprec, pcol, cin, counters, batch_state, out, ts, tag, true,
+  phase_c_passes(sc, cam, W, maxrec, dep_pix, deprec, pcol, cin, counters, batch_state, out, patch, ts, tag, true,
                  zero);
   flush_events(zero, zcount);
 }
@@ -1542,7 +1662,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_
     Scene sc, Cam cam, int W, int H, int maxrec, const uint8_t* __restrict__ cls,
     const long long* __restrict__ dep_pix, const DepRec* __restrict__ deprec,
     const float4* __restrict__ pcol, CinG* __restrict__ cin, int* __restrict__ counters,
-    int* __restrict__ batch_state, uint8_t* __restrict__ out,
+    int* __restrict__ batch_state, uint8_t* __restrict__ out, uint32_t* __restrict__ patch,
     unsigned long long* __restrict__ zcount, TeamState* __restrict__ ts, unsigned tag,
     int tiles) {
   __shared__ StageBuf<kStage> stage;
@@ -1555,7 +1675,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_
     shade_tile(sc, cam, W, H, maxrec, t, cls, out, zero);
     if ((threadIdx.x & 63) == 0) atomicAdd(&counters[10], 1);
   }
-  phase_c_passes(sc, cam, W, maxrec, dep_pix, deprec, pcol, cin, counters, batch_state, out, ts, tag, false,
+  phase_c_passes(sc, cam, W, maxrec, dep_pix, deprec, pcol, cin, counters, batch_state, out, patch, ts, tag, false,
                  zero);
   flush_events(zero, zcount);
 }
@@ -1574,7 +1694,7 @@ template <bool kStage>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_FINISH_WAVES))) k_dep_chunks(
     Scene sc, Cam cam, int W, int maxrec, const long long* __restrict__ dep_pix,
     const DepRec* __restrict__ deprec, const float4* __restrict__ pcol, CinG* __restrict__ cin,
-    const int* __restrict__ counters, uint8_t* __restrict__ out,
+    const int* __restrict__ counters, uint8_t* __restrict__ out, uint32_t* __restrict__ patch,
     unsigned long long* __restrict__ zcount, TeamState* __restrict__ ts, unsigned tag) {
   __shared__ StageBuf<kStage> stage;
   __shared__ int s_j[kChunk];
@@ -1600,7 +1720,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_
       if (in && !hv) {
         const long long p = dep_pix[j];
         const float4 k = pcol[p];
-        store_rgb(out + (size_t)p * 3, v3(k.x, k.y, k.z));
+        store_dep(out, patch, p, j, v3(k.x, k.y, k.z));
       }
       const unsigned long long m = __ballot(hv);
       int base = 0;
@@ -1631,7 +1751,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_
         shoot<kModeParityC>(sc, d, maxrec, c, po, zero);
         rgb = po.rgb;
       }
-      store_rgb(out + (size_t)p * 3, rgb);
+      store_dep(out, patch, p, j, rgb);
     }
     __syncthreads();   // the list is rebuilt for the next chunk
   }
@@ -1669,7 +1789,7 @@ static Cam make_cam(const LaunchScene& s, int W, int H) {
 hipError_t launch_render(const LaunchScene& s, int W, int H, int row0, int row_step, int nrows,
                          int maxrec, uint8_t* out, unsigned long long* zcount,
                          hipStream_t stream) {
-  dim3 grid((W + kTile - 1) / kTile, (nrows + kTile - 1) / kTile);
+  dim3 grid((W + kTileW - 1) / kTileW, (nrows + kTileH - 1) / kTileH);
   hipLaunchKernelGGL(stage_fits(s) ? k_render<true> : k_render<false>, grid, dim3(kBlock), 0, stream, make_scene(s), make_cam(s, W, H),
                      W, H, row0, row_step, nrows, maxrec, out, zcount);
   return hipGetLastError();
@@ -1687,7 +1807,7 @@ hipError_t launch_parity(const LaunchScene& s, int W, int H, int maxrec, uint8_t
   const Scene sc = make_scene(s);
   const Cam cam = make_cam(s, W, H);
   const bool st = stage_fits(s);
-  dim3 grid((W + kTile - 1) / kTile, (H + kTile - 1) / kTile);
+  dim3 grid((W + kTileW - 1) / kTileW, (H + kTileH - 1) / kTileH);
   if (w.side && w.split_shade)   // carry part only; colours shaded beside the resolver (k_side)
     hipLaunchKernelGGL(st ? k_classify<true> : k_classify<false>, grid, dim3(kBlock), 0, stream, sc, cam, W, H, maxrec, w.cls,
                        w.wcarry, (DepRec*)w.deprec);
@@ -1738,7 +1858,7 @@ hipError_t launch_parity(const LaunchScene& s, int W, int H, int maxrec, uint8_t
                        W, H, maxrec, w.cls, w.dep_pix, (const DepRec*)w.deprec, w.wcarry,
                        (CinG*)w.cin, w.counters,
                        w.batch_state,
-                       out, zcount, (TeamState*)w.team, w.resolve_blocks, w.epoch,
+                       out, w.patch, zcount, (TeamState*)w.team, w.resolve_blocks, w.epoch,
                        w.split_shade);
     (void)hipEventRecord(w.join, w.side);
   }
@@ -1764,13 +1884,13 @@ static void enqueue_phase_c(const Scene& sc, const Cam& cam, bool st, int W, int
     hipLaunchKernelGGL(st ? k_finish<true> : k_finish<false>, dim3(w.phase_c_blocks), dim3(kBlock), 0, stream, sc, cam, W, H,
                        maxrec, w.cls, w.dep_pix, (const DepRec*)w.deprec, w.wcarry,
                        (CinG*)w.cin, w.counters, w.batch_state,
-                       out,
+                       out, w.patch,
                        zcount, (TeamState*)w.team, w.epoch, (w.side && w.split_shade) ? 1 : 0);
   } else {   // all of phase C after the resolver: clean entries, then full waves of the rest
     hipLaunchKernelGGL(st ? k_dep_chunks<true> : k_dep_chunks<false>, dim3(w.phase_c_blocks),
                        dim3(kBlock), 0, stream, sc, cam, W, maxrec, w.dep_pix,
                        (const DepRec*)w.deprec, (const float4*)w.wcarry, (CinG*)w.cin,
-                       w.counters, out, zcount, (TeamState*)w.team, w.epoch);
+                       w.counters, out, w.patch, zcount, (TeamState*)w.team, w.epoch);
   }
 }
 
