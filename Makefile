@@ -25,8 +25,8 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off \
             -Wno-c11-extensions -Wno-unused-result
 CFLAGS   := -O3 -ffp-contract=off -fPIC -Wall -Wno-unused-result -Iinclude -I$(SRC)
 
-HIP_SRCS  := $(SRC)/rc_kernels.hip $(SRC)/rc_api.hip
-HIP_HDRS  := $(SRC)/rc_device.hpp $(SRC)/rc_kernels.h $(SRC)/rc_scene.h include/raycast_hip.h
+HIP_SRCS  := $(SRC)/rc_kernels.hip $(SRC)/rc_api.hip $(SRC)/rc_shard.hip
+HIP_HDRS  := $(SRC)/rc_device.hpp $(SRC)/rc_kernels.h $(SRC)/rc_runtime.h $(SRC)/rc_scene.h include/raycast_hip.h
 FRONT_SRC := $(SRC)/front/parse.c $(SRC)/front/objects.c $(SRC)/front/ppm.c
 
 .PHONY: all oracle ref clean stamps
@@ -40,8 +40,11 @@ $(OBJ)/rc_scene.o: $(SRC)/rc_scene.c $(SRC)/rc_scene.h include/raycast_hip.h
 	@mkdir -p $(OBJ)
 	$(CC) $(CFLAGS) -c $< -o $@
 
-$(LIB)/libraycast_hip.so: $(OBJ)/rc_kernels.o $(OBJ)/rc_api.o $(OBJ)/rc_scene.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -o $@ -lpthread
+ROCM    ?= /opt/rocm
+HIPLIBS := -L$(ROCM)/lib -lrccl -Wl,-rpath,$(ROCM)/lib -lpthread
+
+$(LIB)/libraycast_hip.so: $(OBJ)/rc_kernels.o $(OBJ)/rc_api.o $(OBJ)/rc_shard.o $(OBJ)/rc_scene.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -o $@ $(HIPLIBS)
 
 $(LIB)/libraycast_front.so: $(FRONT_SRC) include/raycast_hip.h
 	@mkdir -p $(LIB)
@@ -59,8 +62,8 @@ $(OBJ)/stamps_kernels.o: $(SRC)/rc_kernels.hip $(HIP_HDRS)
 $(OBJ)/stamps_api.o: $(SRC)/rc_api.hip $(HIP_HDRS)
 	@mkdir -p $(OBJ)
 	$(HIPCC) $(HIPFLAGS) -DRC_STAMPS=1 -c $< -o $@
-$(LIB)/libraycast_hip_stamps.so: $(OBJ)/stamps_kernels.o $(OBJ)/stamps_api.o $(OBJ)/rc_scene.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -o $@ -lpthread
+$(LIB)/libraycast_hip_stamps.so: $(OBJ)/stamps_kernels.o $(OBJ)/stamps_api.o $(OBJ)/rc_shard.o $(OBJ)/rc_scene.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -o $@ $(HIPLIBS)
 
 oracle:
 	$(MAKE) -C oracle oracle
@@ -79,5 +82,5 @@ $(OBJ)/coalesced_kernels.o: $(SRC)/rc_kernels.hip $(HIP_HDRS)
 	$(HIPCC) $(HIPFLAGS) -DRC_TILE_W=32 -DRC_TILE_STAGE=1 -c $< -o $@
 $(OBJ)/t16_kernels.o: $(SRC)/rc_kernels.hip $(HIP_HDRS)
 	$(HIPCC) $(HIPFLAGS) -DRC_TILE_W=16 -DRC_TILE_STAGE=1 -c $< -o $@
-$(LIB)/libraycast_hip_%.so: $(OBJ)/%_kernels.o $(OBJ)/rc_api.o $(OBJ)/rc_scene.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -o $@ -lpthread
+$(LIB)/libraycast_hip_%.so: $(OBJ)/%_kernels.o $(OBJ)/rc_api.o $(OBJ)/rc_shard.o $(OBJ)/rc_scene.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -o $@ $(HIPLIBS)

@@ -120,7 +120,7 @@ _Static_assert(sizeof(light_t) == 72, "light_t must match C/objects.h layout");
  * row-major, top row first).  Options come from the environment:
  *   RAYCAST_MODE   = parity (default) | fast
  *   RAYCAST_DEPTH  = bounce depth d, MAX_RECURSION = d+1 (default 6 == C/raycast.c:14)
- *   RAYCAST_GPUS   = number of GPUs for row-cyclic sharding (default 1)
+ *   RAYCAST_GPUS   = number of GPUs for row-cyclic sharding over RCCL (default 1; both modes)
  *   RAYCAST_DEVICE = first HIP device ordinal (default 0)
  *   RAYCAST_STATS  = 1: one JSON metrics line on stderr
  * Any HIP failure prints a message to stderr and exit(1)s (reference error convention). */
@@ -212,6 +212,58 @@ typedef struct rc_phase_stats {
 } rc_phase_stats;
 int rc_profile_begin(void);
 int rc_profile_end(rc_phase_stats *out);
+
+/* ---- multi-GPU row shards ----------------------------------------------
+ * Rows are dealt cyclically (image row y -> rank y % G).  Every rank renders its rows; the
+ * root (rank 0) gathers the row blocks over RCCL (ncclGather over xGMI) and undoes the
+ * interleave on its device.  Parity mode adds the carry chain's exchange: every rank runs
+ * phase A on its rows, the root gathers the DEP entries (ncclSend/ncclRecv), resolves the
+ * scan-order carry chain and sends each rank its carry-ins back for phase C.  The output is
+ * byte-identical to rc_render on one device. */
+#define RC_GROUP_ID_BYTES 128          /* == sizeof(ncclUniqueId) */
+enum { RC_XFER_AUTO = 0,   /* RCCL when every rank has its own device, else RC_XFER_COPY */
+       RC_XFER_RCCL = 1,   /* RCCL communicators (xGMI)                                 */
+       RC_XFER_COPY = 2    /* device copies between the ranks' buffers (one process)    */ };
+typedef struct rc_group rc_group;
+
+/* A fresh RCCL unique id: rank 0 of a multi-process job makes one and shares it. */
+int rc_group_unique_id(unsigned char id[RC_GROUP_ID_BYTES]);
+/* One rank of a multi-process job (one process per GPU) on `device`; collective over the
+ * nranks processes (ncclCommInitRank).  NULL on failure. */
+rc_group *rc_group_create_rank(int nranks, int rank, const unsigned char id[RC_GROUP_ID_BYTES],
+                               int device);
+/* All nranks ranks in this process, rank i on devices[i] (ranks may share a device only with
+ * RC_XFER_COPY; RC_XFER_AUTO picks).  NULL on failure. */
+rc_group *rc_group_create_local(int nranks, const int *devices, int transport);
+void rc_group_destroy(rc_group *group);
+int rc_group_size(const rc_group *group);
+int rc_group_transport(const rc_group *group);   /* RC_XFER_RCCL or RC_XFER_COPY */
+
+/* Render W x H row-sharded over the group: collective (every rank's process calls it with
+ * the same arguments).  The image lands in d_image (W*H*3 bytes, device memory of rank 0's
+ * device; NULL = a buffer of the group's own) on the root; other ranks ignore d_image.
+ * Synchronous.  timing (may be NULL): total_ms (host), kernel_ms (root's device span),
+ * resolve_ms, dep_pixels and zero_normalize of the whole image (root).  Returns 0 on
+ * success. */
+int rc_render_sharded(rc_group *group, const rc_scene *scene, int width, int height,
+                      const rc_options *opt, uint8_t *d_image, rc_timing *timing);
+
+typedef struct rc_shard_stats {   /* the last rc_render_sharded, on the root */
+  int ranks;
+  double total_ms;        /* host wall clock of the call                                   */
+  double device_ms;       /* root's stream: first kernel to the de-interleaved image        */
+  double local_ms;        /* root's own rows: fast: render; parity: phase A + packing       */
+  double exchange_in_ms;  /* parity: end of the root's phase A to the resolver's start      */
+  double resolve_ms;      /* parity: image-wide carry resolver on the root                  */
+  double phase_c_ms;      /* parity: resolver end to the end of the root's phase C          */
+  double image_ms;        /* row-block gather + de-interleave                               */
+  int64_t dep_pixels;
+  int64_t zero_normalize;
+  int64_t entry_bytes;    /* DEP entries moved to the root                                  */
+  int64_t carry_bytes;    /* carry-ins moved back                                           */
+  int64_t image_bytes;    /* row blocks moved to the root (padded to ceil(H/G) rows)        */
+} rc_shard_stats;
+int rc_group_last_stats(const rc_group *group, rc_shard_stats *out);
 
 /* Library version / build string. */
 const char *rc_version(void);

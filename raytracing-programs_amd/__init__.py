@@ -71,13 +71,25 @@ class RcPhaseStats(ctypes.Structure):
                 ("total_ms", ctypes.c_double)]
 
 
+class RcShardStats(ctypes.Structure):
+    _fields_ = [("ranks", ctypes.c_int), ("total_ms", ctypes.c_double),
+                ("device_ms", ctypes.c_double), ("local_ms", ctypes.c_double),
+                ("exchange_in_ms", ctypes.c_double), ("resolve_ms", ctypes.c_double),
+                ("phase_c_ms", ctypes.c_double), ("image_ms", ctypes.c_double),
+                ("dep_pixels", ctypes.c_int64), ("zero_normalize", ctypes.c_int64),
+                ("entry_bytes", ctypes.c_int64), ("carry_bytes", ctypes.c_int64),
+                ("image_bytes", ctypes.c_int64)]
+
+
 assert ctypes.sizeof(ShapeT) == 104 and ctypes.sizeof(LightT) == 72
 
 # the functions include/raycast_hip.h declares, per library
 HIP_EXPORTS = ["raycast", "rc_default_options", "rc_scene_create", "rc_scene_destroy",
                "rc_scene_parity_defined", "rc_render", "rc_render_device", "rc_last_kernel_ms",
                "rc_profile_begin", "rc_profile_end", "rc_version", "rc_frame_submit",
-               "rc_frames_wait", "rc_pipe_reset"]
+               "rc_frames_wait", "rc_pipe_reset", "rc_group_unique_id", "rc_group_create_rank",
+               "rc_group_create_local", "rc_group_destroy", "rc_group_size",
+               "rc_group_transport", "rc_render_sharded", "rc_group_last_stats"]
 FRONT_EXPORTS = ["add_new_sphere", "add_new_plane", "add_new_quadric", "free_shape_list",
                  "free_light_list", "add_new_spot_light", "add_new_point_light", "parse_json",
                  "set_to_black", "ppm_WriteOutP3", "ppm_clamp"]
@@ -125,6 +137,18 @@ def hip_lib():
     lib.rc_version.restype = ctypes.c_char_p
     lib.rc_default_options.argtypes = [ctypes.POINTER(RcOptions), ctypes.c_int]
     lib.rc_profile_end.argtypes = [ctypes.POINTER(RcPhaseStats)]
+    lib.rc_group_unique_id.argtypes = [ctypes.c_char_p]
+    lib.rc_group_create_rank.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
+    lib.rc_group_create_rank.restype = ctypes.c_void_p
+    lib.rc_group_create_local.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.c_int]
+    lib.rc_group_create_local.restype = ctypes.c_void_p
+    lib.rc_group_destroy.argtypes = [ctypes.c_void_p]
+    lib.rc_group_size.argtypes = [ctypes.c_void_p]
+    lib.rc_group_transport.argtypes = [ctypes.c_void_p]
+    lib.rc_render_sharded.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                      ctypes.POINTER(RcOptions), ctypes.c_void_p,
+                                      ctypes.POINTER(RcTiming)]
+    lib.rc_group_last_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(RcShardStats)]
     return lib
 
 
@@ -309,6 +333,78 @@ def version():
 
 
 # ------------------------------------------------------------- multi-GPU row shards --
+XFER = {"auto": 0, "rccl": 1, "copy": 2}
+GROUP_ID_BYTES = 128
+
+
+class Group:
+    """Row-sharded rendering over several GPUs (rc_group / rc_render_sharded):
+    row y -> rank y % G, RCCL gathers to rank 0; parity adds the DEP-entry gather, the
+    carry resolver on the root and the carry-in scatter.  `Group.local([0, 1, 2])` drives all
+    ranks from this process; `Group.rank(world, rank, uid, device)` is one rank of a
+    one-process-per-GPU job (uid from `Group.unique_id()` on rank 0, shared by the caller)."""
+
+    def __init__(self, handle):
+        if not handle:
+            raise RuntimeError("rc_group creation failed (see stderr)")
+        self._h = handle
+
+    @staticmethod
+    def unique_id():
+        buf = ctypes.create_string_buffer(GROUP_ID_BYTES)
+        if hip_lib().rc_group_unique_id(buf) != 0:
+            raise RuntimeError("rc_group_unique_id failed")
+        return buf.raw
+
+    @classmethod
+    def local(cls, devices, transport="auto"):
+        arr = (ctypes.c_int * len(devices))(*devices)
+        return cls(hip_lib().rc_group_create_local(len(devices), arr, XFER[transport]))
+
+    @classmethod
+    def rank(cls, world, rank, uid, device):
+        assert len(uid) == GROUP_ID_BYTES
+        return cls(hip_lib().rc_group_create_rank(world, rank, uid, device))
+
+    @property
+    def size(self):
+        return hip_lib().rc_group_size(self._h)
+
+    @property
+    def transport(self):
+        return {1: "rccl", 2: "copy"}[hip_lib().rc_group_transport(self._h)]
+
+    def render(self, scene, width, height, d_image_ptr=None, depth=6, mode="parity",
+               timing=None):
+        """Collective render; the root's image lands at d_image_ptr (W*H*3 B on rank 0's
+        device)."""
+        opt = options(depth, mode)
+        t = RcTiming()
+        rc = hip_lib().rc_render_sharded(self._h, scene.packed(), width, height, ctypes.byref(opt),
+                                         ctypes.c_void_p(d_image_ptr or 0), ctypes.byref(t))
+        if rc != 0:
+            raise RuntimeError("rc_render_sharded failed (see stderr)")
+        if timing is not None:
+            timing.update({k: getattr(t, k) for k, _ in RcTiming._fields_})
+
+    def stats(self):
+        st = RcShardStats()
+        if hip_lib().rc_group_last_stats(self._h, ctypes.byref(st)) != 0:
+            raise RuntimeError("rc_group_last_stats failed")
+        return {k: getattr(st, k) for k, _ in RcShardStats._fields_}
+
+    def close(self):
+        if self._h:
+            hip_lib().rc_group_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def row_shard(height, rank, world):
     """Rows of rank `rank` under the row-cyclic partition (row y -> rank y % world):
     (row0, row_step, nrows).  Contiguous blocks are 1.7-2.1x imbalanced on the reference

@@ -5,11 +5,7 @@
 // photo_data.pixmap.  Per-device state (stream, events, grow-only workspaces) is created on
 // first use and kept for the life of the process, so repeated renders allocate nothing.
 //
-// Multi-GPU inside one process (RAYCAST_GPUS=N, fast mode): one host thread per device,
-// rows dealt cyclically (row r -> device r mod N; contiguous blocks are 1.7-2.1x imbalanced,
-// SURVEY.md §5), each device renders its rows into a compact buffer and a strided 2-D copy
-// drops them straight into their interleaved place in the host pixmap.  The multi-process
-// (one rank per GPU, RCCL gather) path is driven from Python: see bench.py.
+// Multi-GPU (RAYCAST_GPUS=N, both modes): row shards over RCCL, rc_shard.hip.
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
@@ -27,126 +23,12 @@
 
 #include "raycast_hip.h"
 #include "rc_kernels.h"
+#include "rc_runtime.h"
 #include "rc_scene.h"
 
 #define RC_VERSION "raycast-mi355x 0.1 (gfx950)"
 
-namespace {
-
-#define HIP_TRY(expr)                                                                   \
-  do {                                                                                  \
-    hipError_t e_ = (expr);                                                             \
-    if (e_ != hipSuccess) {                                                             \
-      std::fprintf(stderr, "Error: HIP call failed: %s (%s) at %s:%d\n", #expr,        \
-                   hipGetErrorString(e_), __FILE__, __LINE__);                          \
-      return -1;                                                                        \
-    }                                                                                   \
-  } while (0)
-
-constexpr int kMaxDevices = 16;
-
-struct DevBuf {
-  void* p = nullptr;
-  size_t bytes = 0;
-  int ensure(size_t need) {
-    if (need <= bytes) return 0;
-    if (p) (void)hipFree(p);
-    p = nullptr;
-    bytes = 0;
-    if (hipMalloc(&p, need) != hipSuccess) return -1;
-    bytes = need;
-    return 0;
-  }
-};
-
-// One frame's device state: the uploaded scene, the zero-normalize counter and the parity
-// workspace.  The plain path has one (DevCtx::fb); pipelined frames alternate two (Pipe).
-struct FrameBufs {
-  unsigned epoch = 0;   // carry-in tag of the last parity frame in this workspace
-  DevBuf zcount;        // zero-normalize counter
-  DevBuf scene;         // uploaded packed scene
-  const void* scene_src = nullptr;   // host image last uploaded
-  DevBuf cls, wcarry, deprec, rows, dep_pix, seg_key, seg_start, seg_order, batch_state, cin,
-      counters, team, trace;
-};
-
-// Pipelined parity frames (rc_frame_submit).  The device's CUs are split in two partitions
-// (hipExtStreamCreateWithCUMask).  Partition A runs the carry resolvers: kLanes resolver
-// streams, each resolver grid sized to A/kLanes CUs (one workgroup per CU), so the resolvers in
-// flight are always wholly resident side by side (a team spins on co-resident workgroups;
-// at most kLanes resolvers are in flight since each stream runs its resolvers in order).
-// Partition B runs the pixel phases: the frames' phase A one at a time in submission order
-// (each waits for the previous frame's, adone), so the frame whose resolver comes next always
-// has the whole partition; two streams (pix[0], pix[1]) alternate so a frame's compaction —
-// a chain of small latency-bound kernels — overlaps the next frame's phase A; each lane's
-// phase C runs on a stream of its own (pc[lane], after the frame's resolver); a slot's next
-// phase A waits for the slot's previous phase C (cdone).  A resolver is
-// latency-bound (its carry chains), so overlapping kLanes of them multiplies the frame rate
-// until partition B's pixel work becomes the bound.  (RC_PIPE_SLOTSTREAMS: the earlier form,
-// one stream per slot running A, compaction and C in turn.)
-struct Pipe {
-  static constexpr int kSlots = 8;   // frame workspaces (a frame re-uses slot k after k's end)
-  static constexpr int kLanes = 4;   // resolvers in flight (at most)
-  bool init = false;
-  int res_cus = 0;                   // CUs in partition A
-  int lanes = 2;                     // resolver streams in use (RC_PIPE_RESOLVERS)
-  int slots = 4;                     // workspaces / pixel streams in use (RC_PIPE_SLOTS)
-  hipStream_t pix[kSlots] = {}, res[kLanes] = {};
-  hipEvent_t ready[kSlots] = {}, done[kSlots] = {};
-  bool fifo = true;                  // pa = pix[0] + pc[] (false: RC_PIPE_SLOTSTREAMS)
-  hipStream_t pc[kLanes] = {};
-  hipEvent_t cdone[kSlots] = {};
-  bool cpend[kSlots] = {};           // slot k's phase C is enqueued and not yet synchronised
-  hipEvent_t adone[kSlots] = {};     // after slot k's phase A
-  static constexpr int kEv = 64;     // resolver timing events of the last kEv frames
-  hipEvent_t rt[kEv][2] = {};
-  FrameBufs fb[kSlots];
-  long long submitted = 0;           // parity frames since the last rc_frames_wait
-  long long frames = 0;              // frames of any mode since the last rc_frames_wait
-  long long total = 0;               // parity frames ever (slot / stream rotation)
-  long long last = -1;               // slot of the last parity frame
-  bool used[kSlots] = {};
-  bool rt_on = true;                 // resolver timing events recorded (RC_PIPE_NO_RT: off)
-};
-
-struct DevCtx {
-  bool init = false;
-  int device = 0;
-  hipStream_t side = nullptr;   // phase C's side stream
-  hipEvent_t fork = nullptr, join = nullptr;
-  int side_blocks = 0, side_lds = 0;
-  int cus = 256;
-  hipStream_t stream = nullptr;
-  // event sets: [0] start, then per phase ends (fast: [1] = render; parity: [1] phase A,
-  // [2] compaction, [3] resolver, [4] phase C).  Set 0 serves plain calls; inside an
-  // rc_profile_begin/end window every call takes the next set of the pool.
-  static constexpr int kEvSets = 64;
-  hipEvent_t ev[kEvSets][5] = {};
-  int prof_active = 0, prof_calls = 0, prof_parity = 0;
-  DevBuf out;          // rc_render output pixmap
-  uint8_t* stage[2] = {nullptr, nullptr};   // pinned bounce buffers of copy_to_host
-  hipEvent_t stage_ev[2] = {nullptr, nullptr};
-  FrameBufs fb;        // scene, counter and parity workspace of the plain path
-  Pipe pipe;
-  int resident_blocks = 0;
-  int resident_lds = -1;
-  static constexpr int kResCache = 4;   // resident resolver grids per LDS reservation
-  int res_lds[kResCache] = {};
-  int res_blocks[kResCache] = {};
-  size_t parity_pixels = 0;
-  int parity_rows = 0;
-  // rc_render's overlapped copy (parity): the framebuffer leaves on `d2h` while the resolver
-  // runs, then only the DEP entries' colours (`patch`, packed RGB per entry) follow
-  hipStream_t d2h = nullptr;
-  DevBuf patch;
-  uint8_t* pin_pix = nullptr;     // pinned: DEP pixel indices (int64 per entry)
-  uint8_t* pin_patch = nullptr;   // pinned: DEP entries' packed RGB
-  size_t pin_bytes = 0;           // capacity of each pinned buffer, in entries
-  int* pin_cnt = nullptr;         // pinned: counters[0..3]
-  // One render at a time per device: the workspace, TeamState, events and streams above are
-  // shared by every call on this device (rc_render, rc_render_device, rc_frame_submit).
-  std::mutex mu;
-};
+namespace rcrt {
 
 DevCtx g_ctx[kMaxDevices];
 std::mutex g_ctx_mu;
@@ -342,12 +224,10 @@ int copy_overlapped(DevCtx& c, uint8_t* host, const uint8_t* dev, size_t bytes,
   return 0;
 }
 
-}  // namespace
+}  // namespace rcrt
 
-// ------------------------------------------------------------------- scene object --
-struct rc_scene {
-  rc_packed_header* img;   // host packed image
-};
+using namespace rcrt;
+
 
 extern "C" {
 
@@ -401,7 +281,7 @@ int rc_scene_parity_defined(const rc_scene* s) { return s ? s->img->phantom_defi
 
 }  // extern "C"
 
-namespace {
+namespace rcrt {
 
 int upload_scene(FrameBufs& b, hipStream_t stream, const rc_scene* s, rc::LaunchScene& ls) {
   const rc_packed_header* h = s->img;
@@ -749,7 +629,7 @@ void fill_device_timing(DevCtx& c, const rc_options* opt, rc_timing* t) {
   }
 }
 
-}  // namespace
+}  // namespace rcrt
 
 extern "C" {
 
@@ -1052,103 +932,65 @@ int rc_render(const rc_scene* s, int W, int H, const rc_options* opt, uint8_t* p
     return -1;
   }
   if (G > ndev - opt->device) G = ndev - opt->device;
+  if (G > rc::kMaxShards) G = rc::kMaxShards;
   if (G > H) G = H;
   const bool parity = opt->mode == RC_MODE_PARITY && opt->max_recursion > 1;
-  if (parity) G = 1;   // the scan-order carry chain is resolved on one device
   const size_t row_bytes = (size_t)W * 3;
-  std::vector<int> rcodes(G, 0);
-  std::vector<rc_timing> tims(G);
-  auto work = [&](int g) {
-    const int dev = opt->device + g;
+  if (G > 1) {   // row shards over RCCL (rc_shard.hip), the image on the first device
+    uint8_t* d_image = nullptr;
+    rc_timing tg;
+    if (render_local_group(opt->device, G, s, W, H, opt, &d_image, &tg)) return -1;
     DevCtx* c;
-    if (hipSetDevice(dev) != hipSuccess || ctx_get(dev, &c)) {
-      rcodes[g] = -1;
-      return;
-    }
-    const int nrows = (H - g + G - 1) / G;
-    if (nrows <= 0) return;
-    if (c->out.ensure((size_t)nrows * row_bytes)) {
-      rcodes[g] = -1;
-      return;
-    }
-    uint8_t* d_out = (uint8_t*)c->out.p;
+    if (hipSetDevice(opt->device) != hipSuccess || ctx_get(opt->device, &c)) return -1;
     std::lock_guard<std::mutex> lk(c->mu);
-    // parity, one device: the copy overlaps the resolver (copy_overlapped); split shading
-    // leaves the non-DEP colours to phase C, so its framebuffer is not final after phase A
-    const bool overlap = G == 1 && parity && !std::getenv("RC_SPLIT_SHADE") &&
-                         !std::getenv("RC_SERIAL_D2H");
-    uint32_t* patch = nullptr;
-    if (overlap) {
-      if ((!c->d2h && hipStreamCreateWithFlags(&c->d2h, hipStreamNonBlocking) != hipSuccess) ||
-          c->patch.ensure((size_t)W * H * sizeof(uint32_t))) {
-        rcodes[g] = -1;
-        return;
-      }
-      patch = (uint32_t*)c->patch.p;
-    }
-    hipEvent_t* ev = nullptr;
-    if (enqueue_render(*c, s, W, H, g, G, nrows, opt, d_out, c->stream, true, patch, &ev)) {
-      rcodes[g] = -1;
-      return;
-    }
-    if (G == 1) {
-      prefault(pixmap, (size_t)H * row_bytes);
-    } else if (!std::getenv("RC_NO_PREFAULT")) {
-      volatile uint8_t* p = pixmap + (size_t)g * row_bytes;
-      const size_t span = ((size_t)(nrows - 1) * G + 1) * row_bytes;
-      for (size_t o = 0; o < span; o += 4096) p[o] = 0;
-      if (span) p[span - 1] = 0;
-    }
+    prefault(pixmap, (size_t)H * row_bytes);
     auto td = std::chrono::steady_clock::now();
-    if (overlap) {
-      if (copy_overlapped(*c, pixmap, d_out, (size_t)H * row_bytes, ev)) {
-        rcodes[g] = -1;
-        return;
-      }
-    } else if (G == 1) {   // contiguous image: staged, multi-threaded copy
-      if (copy_to_host(*c, pixmap, d_out, (size_t)H * row_bytes, c->stream)) {
-        rcodes[g] = -1;
-        return;
-      }
-    } else {
-      hipError_t e = hipMemcpy2DAsync(pixmap + (size_t)g * row_bytes, row_bytes * G, d_out,
-                                      row_bytes, row_bytes, nrows, hipMemcpyDeviceToHost,
-                                      c->stream);
-      if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-      if (e != hipSuccess) {
-        std::fprintf(stderr, "Error: HIP copy failed: %s\n", hipGetErrorString(e));
-        rcodes[g] = -1;
-        return;
-      }
+    if (copy_to_host(*c, pixmap, d_image, (size_t)H * row_bytes, c->stream)) return -1;
+    if (timing) {
+      *timing = tg;
+      timing->d2h_ms =
+          std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - td).count();
+      timing->total_ms =
+          std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     }
-    if (check_spin_error(c->fb, opt)) {
-      rcodes[g] = -1;
-      return;
-    }
-    std::memset(&tims[g], 0, sizeof(rc_timing));
-    fill_device_timing(*c, opt, &tims[g]);
-    tims[g].d2h_ms =
-        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - td).count();
-  };
-  if (G == 1) {
-    work(0);
-  } else {
-    std::vector<std::thread> th;
-    for (int g = 0; g < G; ++g) th.emplace_back(work, g);
-    for (auto& t : th) t.join();
+    g_last_kernel_ms = tg.resolve_ms > 0.0 ? tg.resolve_ms : tg.kernel_ms;
+    return 0;
   }
-  for (int g = 0; g < G; ++g)
-    if (rcodes[g]) return -1;
+  // one device
+  const int dev = opt->device;
+  DevCtx* c;
+  if (hipSetDevice(dev) != hipSuccess || ctx_get(dev, &c)) return -1;
+  if (c->out.ensure((size_t)H * row_bytes)) return -1;
+  uint8_t* d_out = (uint8_t*)c->out.p;
+  std::lock_guard<std::mutex> lk(c->mu);
+  // parity: the copy overlaps the resolver (copy_overlapped); split shading leaves the non-DEP
+  // colours to phase C, so its framebuffer is not final after phase A
+  const bool overlap = parity && !std::getenv("RC_SPLIT_SHADE") && !std::getenv("RC_SERIAL_D2H");
+  uint32_t* patch = nullptr;
+  if (overlap) {
+    if ((!c->d2h && hipStreamCreateWithFlags(&c->d2h, hipStreamNonBlocking) != hipSuccess) ||
+        c->patch.ensure((size_t)W * H * sizeof(uint32_t)))
+      return -1;
+    patch = (uint32_t*)c->patch.p;
+  }
+  hipEvent_t* ev = nullptr;
+  if (enqueue_render(*c, s, W, H, 0, 1, H, opt, d_out, c->stream, true, patch, &ev)) return -1;
+  prefault(pixmap, (size_t)H * row_bytes);
+  auto td = std::chrono::steady_clock::now();
+  if (overlap) {
+    if (copy_overlapped(*c, pixmap, d_out, (size_t)H * row_bytes, ev)) return -1;
+  } else if (copy_to_host(*c, pixmap, d_out, (size_t)H * row_bytes, c->stream)) {
+    return -1;
+  }
+  if (check_spin_error(c->fb, opt)) return -1;
   if (timing) {
-    for (int g = 0; g < G; ++g) {
-      if (tims[g].kernel_ms > timing->kernel_ms) timing->kernel_ms = tims[g].kernel_ms;
-      if (tims[g].resolve_ms > timing->resolve_ms) timing->resolve_ms = tims[g].resolve_ms;
-      if (tims[g].d2h_ms > timing->d2h_ms) timing->d2h_ms = tims[g].d2h_ms;
-      timing->dep_pixels += tims[g].dep_pixels;
-      timing->zero_normalize += tims[g].zero_normalize;
-    }
+    fill_device_timing(*c, opt, timing);
+    timing->d2h_ms =
+        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - td).count();
     timing->total_ms =
         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  } else {
+    fill_device_timing(*c, opt, nullptr);
   }
   return 0;
 }

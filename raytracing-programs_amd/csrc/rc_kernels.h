@@ -87,6 +87,31 @@ hipError_t launch_parity(const LaunchScene& s, int W, int H, int maxrec, uint8_t
 hipError_t launch_phase_c(const LaunchScene& s, int W, int H, int maxrec, uint8_t* out,
                           const ParityWork& w, unsigned long long* zcount, hipStream_t stream);
 
+// Row shards (rc_shard.hip; wire formats in rc_kernels.hip).  kMaxShards ranks at most.
+constexpr int kMaxShards = 16;
+size_t shard_entry_bytes();   // one DEP entry on the wire
+size_t shard_row_bytes();     // one row summary on the wire
+// A rank: phase A on rows row0 + k*row_step (k < nrows) into rank-local buffers, the local
+// DEP list (w.dep_pix, local pixels; w.counters[2] = entries) and the wire entries / rows.
+hipError_t launch_shard_local(const LaunchScene& s, int W, int H, int row0, int row_step,
+                              int nrows, int maxrec, uint8_t* out, const ParityWork& w,
+                              void* ent, void* rows, unsigned long long* zcount,
+                              hipStream_t stream);
+// The root: image scan order from the gathered rows ([G][rmax]) and entries (rank g's at
+// offs[g]), the carry resolver, and the carry-ins in the gathered layout (cin_ret).
+// ev (optional): [0] resolver start, [1] resolver end.
+hipError_t launch_shard_resolve(const LaunchScene& s, int W, int H, int G, int rmax,
+                                const void* rows_all, const void* ent_all,
+                                const long long* offs, int maxrec, const ParityWork& w,
+                                void* cin_ret, hipStream_t stream, const hipEvent_t* ev);
+// A rank: phase C of its DEP list once its carry-ins (tag) are in w.cin.
+hipError_t launch_shard_phase_c(const LaunchScene& s, int W, int H, int row0, int row_step,
+                                int maxrec, uint8_t* out, const ParityWork& w, unsigned tag,
+                                unsigned long long* zcount, hipStream_t stream);
+// The root: image <- gathered row blocks [G][rmax][W*3].
+hipError_t launch_deinterleave(const uint8_t* gathered, int G, int rmax, int W, int H,
+                               uint8_t* img, hipStream_t stream);
+
 size_t deprec_bytes();
 size_t row_stats_bytes();
 size_t team_state_bytes();

@@ -211,7 +211,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_
 
 // ------------------------------------------------------------------ parity phase A --
 template <bool kStage>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_PHASE_A_WAVES))) k_phase_a(Scene sc, Cam cam, int W, int H, int maxrec,
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_PHASE_A_WAVES))) k_phase_a(Scene sc, Cam cam, int W, int row0, int row_step, int nrows, int maxrec,
                                                     uint8_t* __restrict__ out,
                                                     uint8_t* __restrict__ cls,
                                                     float4* __restrict__ wcarry,
@@ -224,13 +224,15 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_
   if (!kStage) __syncthreads();
   int lx, ly;
   tile_pixel(lx, ly);
+  // local row y (a shard renders rows row0 + y * row_step of the image; the whole image:
+  // 0, 1, H); every per-pixel buffer is indexed by the local pixel
   const int x0 = blockIdx.x * kTileW, y0 = blockIdx.y * kTileH;
   const int x = x0 + lx;
   const int y = y0 + ly;
-  if (x < W && y < H) {
+  if (x < W && y < nrows) {
     const size_t p = (size_t)y * W + x;
     int zero = 0;
-    const V3 d = primary_dir(cam, x, y, zero);
+    const V3 d = primary_dir(cam, x, row0 + y * row_step, zero);
     PixelOut po;
     shoot<kModeParityA>(sc, d, maxrec, v3(0.0f, 0.0f, 0.0f), po, zero);
     if (RC_TILE_STAGE) ((uint8_t*)tb.cls[ly])[lx] = po.cls;
@@ -254,7 +256,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_
   if (!tile_last_wave(tb)) return;
   const int nx = W - x0 < kTileW ? W - x0 : kTileW;
   auto row_at = [&](uint8_t* base, int q, int bpp) -> uint8_t* {
-    return y0 + q < H ? base + ((size_t)(y0 + q) * W + x0) * bpp : nullptr;
+    return y0 + q < nrows ? base + ((size_t)(y0 + q) * W + x0) * bpp : nullptr;
   };
   tile_write_rows<kTileW * 3 / 4>(tb.rgb, [&](int q) { return row_at(out, q, 3); }, nx * 3);
   tile_write_rows<kTileW / 4>(tb.cls, [&](int q) { return row_at(cls, q, 1); }, nx);
@@ -1692,7 +1694,8 @@ constexpr int kChunk = 1024;
 
 template <bool kStage>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_FINISH_WAVES))) k_dep_chunks(
-    Scene sc, Cam cam, int W, int maxrec, const long long* __restrict__ dep_pix,
+    Scene sc, Cam cam, int W, int row0, int row_step, int maxrec,
+    const long long* __restrict__ dep_pix,
     const DepRec* __restrict__ deprec, const float4* __restrict__ pcol, CinG* __restrict__ cin,
     const int* __restrict__ counters, uint8_t* __restrict__ out, uint32_t* __restrict__ patch,
     unsigned long long* __restrict__ zcount, TeamState* __restrict__ ts, unsigned tag) {
@@ -1745,7 +1748,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_
         const float4 k = pcol[p];
         rgb = shade_dep_cont(sc, deprec[p], maxrec, c, v3(k.x, k.y, k.z), zero);
       } else {
-        const int y = (int)(p / W), x = (int)(p % W);
+        const int y = row0 + (int)(p / W) * row_step, x = (int)(p % W);   // p: local pixel
         const V3 d = primary_dir(cam, x, y, zero);
         PixelOut po;
         shoot<kModeParityC>(sc, d, maxrec, c, po, zero);
@@ -1756,6 +1759,191 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_
     __syncthreads();   // the list is rebuilt for the next chunk
   }
   flush_events(zero, zcount);
+}
+
+// ------------------------------------------------------ row shards (rc_shard.hip) --
+// A parity image split over G ranks by rows (row y -> rank y % G, local row y / G; SURVEY.md
+// §8e).  Every rank runs phase A on its rows into rank-local buffers and packs its DEP entries
+// (k_shard_pack); the root gathers them, rebuilds the image's scan order (k_shard_rows,
+// k_row_scan, k_shard_unpack), resolves the carry chain and sends every rank its entries'
+// carry-ins back (k_shard_cin) for phase C on the rank.  Entries travel in the rank's local
+// scan order, which is the image's scan order restricted to the rank's rows.
+//
+// A DEP entry on the wire: its record (pad = image pixel, pad2 = the last writer pixel before
+// it in the same row, -1 = none) and that writer's carry-out.  A row's summary: the RowStats
+// fields in image pixel indices, the row's first entry in the rank's list and the carry-out of
+// the row's last writer (the key of a segment that starts after this row).
+struct ShardEntry {
+  DepRec rec;
+  float4 kc;
+};
+struct RowShard {
+  int ndep, nstart, loff, pad;
+  long long lastw, lastd, wfirst;
+  float4 cw;
+};
+static_assert(sizeof(ShardEntry) == 64 && sizeof(RowShard) == 64, "wire records");
+
+// One wave per local row: the rank's DEP list (local pixels, phase C's index), its wire
+// entries (at the local DEP offsets of k_row_scan) and the row summary.
+__global__ void __launch_bounds__(256) k_shard_pack(
+    const uint8_t* __restrict__ cls, const float4* __restrict__ wcarry,
+    const DepRec* __restrict__ deprec, int W, int row0, int row_step, int nrows,
+    const int* __restrict__ row_off, long long* __restrict__ dep_pix,
+    ShardEntry* __restrict__ ent, RowShard* __restrict__ rs) {
+  const int y = blockIdx.x * kRowWaves + (int)(threadIdx.x >> 6);
+  if (y >= nrows) return;
+  const int lane = threadIdx.x & 63;
+  const long long lbase = (long long)y * W;
+  const long long gbase = (long long)(row0 + (long long)y * row_step) * W;
+  const unsigned long long lt = lanemask_lt();
+  int l0 = row_off[y], nd = 0, ns = 0;
+  int lw = -1, ld = -1, wf = -1;   // x of the row's last writer / last DEP / first DEP's writer
+  bool first_seen = false;
+  for (int x0 = 0; x0 < W; x0 += 64) {
+    const int x = x0 + lane;
+    const uint8_t c = x < W ? cls[lbase + x] : kClsIdent;
+    const unsigned long long md = __ballot(c == kClsDep), mw = __ballot(c == kClsWriter);
+    const int kw = (mw & lt) ? x0 + hi_bit(mw & lt) : lw;   // in-row writer before the lane
+    const int pd = (md & lt) ? x0 + hi_bit(md & lt) : ld;   // in-row DEP before the lane
+    const bool dep = c == kClsDep;
+    ns += __popcll(__ballot(dep && pd >= 0 && kw > pd));
+    if (!first_seen && md) {
+      const int f = __ffsll((long long)md) - 1;
+      const unsigned long long wb = mw & (f ? (~0ull >> (64 - f)) : 0ull);
+      wf = wb ? x0 + hi_bit(wb) : lw;
+      first_seen = true;
+    }
+    if (dep) {
+      const int l = l0 + __popcll(md & lt);
+      dep_pix[l] = lbase + x;
+      ShardEntry e;
+      e.rec = deprec[lbase + x];
+      e.rec.pad = (int)(gbase + x);
+      e.rec.pad2 = kw >= 0 ? (int)(gbase + kw) : -1;
+      e.kc = kw >= 0 ? wcarry[lbase + kw] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      ent[l] = e;
+    }
+    l0 += __popcll(md);
+    nd += __popcll(md);
+    if (mw) lw = x0 + hi_bit(mw);
+    if (md) ld = x0 + hi_bit(md);
+  }
+  if (lane == 0) {
+    RowShard r;
+    r.ndep = nd;
+    r.nstart = ns;
+    r.loff = row_off[y];
+    r.pad = 0;
+    r.lastw = lw >= 0 ? gbase + lw : -1;
+    r.lastd = ld >= 0 ? gbase + ld : -1;
+    r.wfirst = wf >= 0 ? gbase + wf : -1;
+    r.cw = lw >= 0 ? wcarry[lbase + lw] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    rs[y] = r;
+  }
+}
+
+struct ShardOffs {
+  long long off[kMaxShards];   // first entry of rank g in the gathered entry list
+};
+
+// Root: the image's RowStats from the gathered row summaries ([G][rmax], row y at [y%G][y/G]).
+__global__ void __launch_bounds__(256) k_shard_rows(const RowShard* __restrict__ rsall, int G,
+                                                    int rmax, int H, RowStats* __restrict__ rs) {
+  const int y = blockIdx.x * blockDim.x + threadIdx.x;
+  if (y >= H) return;
+  const RowShard r = rsall[(size_t)(y % G) * rmax + y / G];
+  rs[y] = RowStats{r.ndep, r.nstart, r.lastw, r.lastd, r.wfirst};
+}
+
+// Root, one wave per image row: the row's entries in scan order -> the resolver's inputs.
+// Records are stored densely (entry j at j, dep_pix the identity) and segment keys index a
+// dense carry table (segment s's initial carry at wcarry[s]), so the resolver is unchanged.
+// A segment start is decided exactly as in k_row_compact (writer after the previous DEP).
+__global__ void __launch_bounds__(256) k_shard_unpack(
+    const RowShard* __restrict__ rsall, const ShardEntry* __restrict__ ent, ShardOffs offs,
+    int G, int rmax, int W, int H, const int* __restrict__ row_off,
+    const int* __restrict__ row_soff, const long long* __restrict__ row_prevw,
+    const long long* __restrict__ row_prevd, DepRec* __restrict__ deprec,
+    long long* __restrict__ dep_pix, int* __restrict__ seg_start,
+    long long* __restrict__ seg_key, float4* __restrict__ keycarry) {
+  const int y = blockIdx.x * kRowWaves + (int)(threadIdx.x >> 6);
+  if (y >= H) return;
+  const int lane = threadIdx.x & 63;
+  const int g = y % G;
+  const RowShard r = rsall[(size_t)g * rmax + y / G];
+  const ShardEntry* e = ent + offs.off[g] + r.loff;
+  const int n = r.ndep;
+  const int idx0 = row_off[y];
+  int s0 = row_soff[y];
+  long long pd = row_prevd[y];
+  const long long pw = row_prevw[y];
+  float4 pwc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  if (pw >= 0) {   // the writer before the row is the last writer of its own row
+    const int yw = (int)(pw / W);
+    pwc = rsall[(size_t)(yw % G) * rmax + yw / G].cw;
+  }
+  const unsigned long long lt = lanemask_lt();
+  for (int i0 = 0; i0 < n; i0 += 64) {
+    const int i = i0 + lane;
+    const bool valid = i < n;
+    ShardEntry q;
+    if (valid) q = e[i];
+    const long long pix = valid ? (long long)q.rec.pad : -1;
+    const long long kin = valid ? (long long)q.rec.pad2 : -1;
+    long long prev = __shfl_up(pix, 1, 64);
+    if (lane == 0) prev = pd;
+    const long long kw = kin >= 0 ? kin : pw;
+    const bool st = valid && (prev < 0 || kw > prev);
+    const unsigned long long ms = __ballot(st);
+    if (valid) {
+      const int idx = idx0 + i;
+      deprec[idx] = q.rec;
+      dep_pix[idx] = idx;
+      if (st) {
+        const int s = s0 + __popcll(ms & lt);
+        seg_start[s] = idx;
+        seg_key[s] = kw >= 0 ? s : -1;
+        keycarry[s] = kin >= 0 ? q.kc : pwc;
+      }
+    }
+    s0 += __popcll(ms);
+    const int last = (n - i0 < 64 ? n - i0 : 64) - 1;
+    pd = __shfl(pix, last, 64);
+  }
+}
+
+// Root, one wave per image row: the row's resolved carry-ins, back in the owning rank's list
+// order (the gathered entry list's layout).
+__global__ void __launch_bounds__(256) k_shard_cin(const RowShard* __restrict__ rsall,
+                                                   ShardOffs offs, int G, int rmax, int H,
+                                                   const int* __restrict__ row_off,
+                                                   const CinG* __restrict__ cin,
+                                                   CinG* __restrict__ ret) {
+  const int y = blockIdx.x * kRowWaves + (int)(threadIdx.x >> 6);
+  if (y >= H) return;
+  const int lane = threadIdx.x & 63;
+  const int g = y % G;
+  const RowShard r = rsall[(size_t)g * rmax + y / G];
+  CinG* dst = ret + offs.off[g] + r.loff;
+  const CinG* src = cin + row_off[y];
+  for (int i = lane; i < r.ndep; i += 64) dst[i] = src[i];
+}
+
+// Root: image row y <- gathered[y % G][y / G] (the row-cyclic partition undone).
+__global__ void __launch_bounds__(256) k_deinterleave(const uint8_t* __restrict__ gathered,
+                                                      int G, int rmax, int W, int H,
+                                                      uint8_t* __restrict__ img) {
+  const int y = blockIdx.x;
+  const size_t rb = (size_t)W * 3;
+  const uint8_t* src = gathered + ((size_t)(y % G) * rmax + y / G) * rb;
+  uint8_t* dst = img + (size_t)y * rb;
+  if ((rb & 3) == 0) {
+    for (size_t i = threadIdx.x; i < rb / 4; i += blockDim.x)
+      ((uint32_t*)dst)[i] = ((const uint32_t*)src)[i];
+  } else {
+    for (size_t i = threadIdx.x; i < rb; i += blockDim.x) dst[i] = src[i];
+  }
 }
 
 // ---------------------------------------------------------------------- launchers --
@@ -1812,7 +2000,7 @@ hipError_t launch_parity(const LaunchScene& s, int W, int H, int maxrec, uint8_t
     hipLaunchKernelGGL(st ? k_classify<true> : k_classify<false>, grid, dim3(kBlock), 0, stream, sc, cam, W, H, maxrec, w.cls,
                        w.wcarry, (DepRec*)w.deprec);
   else
-    hipLaunchKernelGGL(st ? k_phase_a<true> : k_phase_a<false>, grid, dim3(kBlock), 0, stream, sc, cam, W, H, maxrec, out,
+    hipLaunchKernelGGL(st ? k_phase_a<true> : k_phase_a<false>, grid, dim3(kBlock), 0, stream, sc, cam, W, 0, 1, H, maxrec, out,
                        w.cls, w.wcarry, (DepRec*)w.deprec, zcount);
   if (ev) (void)hipEventRecord(ev[0], stream);
   if (w.adone) (void)hipEventRecord(w.adone, stream);
@@ -1888,7 +2076,7 @@ static void enqueue_phase_c(const Scene& sc, const Cam& cam, bool st, int W, int
                        zcount, (TeamState*)w.team, w.epoch, (w.side && w.split_shade) ? 1 : 0);
   } else {   // all of phase C after the resolver: clean entries, then full waves of the rest
     hipLaunchKernelGGL(st ? k_dep_chunks<true> : k_dep_chunks<false>, dim3(w.phase_c_blocks),
-                       dim3(kBlock), 0, stream, sc, cam, W, maxrec, w.dep_pix,
+                       dim3(kBlock), 0, stream, sc, cam, W, 0, 1, maxrec, w.dep_pix,
                        (const DepRec*)w.deprec, (const float4*)w.wcarry, (CinG*)w.cin,
                        w.counters, out, w.patch, zcount, (TeamState*)w.team, w.epoch);
   }
@@ -1950,6 +2138,91 @@ int resolve_blocks_resident(int cus, int lds_bytes) {
       per_cu <= 0)
     per_cu = 1;
   return per_cu * cus;
+}
+
+// ----------------------------------------------------------- row-shard launchers --
+size_t shard_entry_bytes() { return sizeof(ShardEntry); }
+size_t shard_row_bytes() { return sizeof(RowShard); }
+
+hipError_t launch_shard_local(const LaunchScene& s, int W, int H, int row0, int row_step,
+                              int nrows, int maxrec, uint8_t* out, const ParityWork& w,
+                              void* ent, void* rows, unsigned long long* zcount,
+                              hipStream_t stream) {
+  const Scene sc = make_scene(s);
+  const Cam cam = make_cam(s, W, H);
+  const bool st = stage_fits(s);
+  (void)hipMemsetAsync(w.counters, 0, 16 * sizeof(int), stream);
+  (void)hipMemsetAsync(w.team, 0, sizeof(TeamState), stream);
+  if (nrows <= 0) return hipGetLastError();
+  dim3 grid((W + kTileW - 1) / kTileW, (nrows + kTileH - 1) / kTileH);
+  hipLaunchKernelGGL(st ? k_phase_a<true> : k_phase_a<false>, grid, dim3(kBlock), 0, stream, sc,
+                     cam, W, row0, row_step, nrows, maxrec, out, w.cls, w.wcarry,
+                     (DepRec*)w.deprec, zcount);
+  const int row_blocks = (nrows + kRowWaves - 1) / kRowWaves;
+  hipLaunchKernelGGL(k_row_stats, dim3(row_blocks), dim3(256), 0, stream, w.cls, W, nrows,
+                     (RowStats*)w.row_stats);
+  hipLaunchKernelGGL(k_row_scan, dim3(1), dim3(1024), 0, stream, nrows,
+                     (const RowStats*)w.row_stats, w.row_off, w.row_soff, w.row_prevw,
+                     w.row_prevd, w.counters);
+  hipLaunchKernelGGL(k_shard_pack, dim3(row_blocks), dim3(256), 0, stream, w.cls, w.wcarry,
+                     (const DepRec*)w.deprec, W, row0, row_step, nrows, w.row_off, w.dep_pix,
+                     (ShardEntry*)ent, (RowShard*)rows);
+  return hipGetLastError();
+}
+
+hipError_t launch_shard_resolve(const LaunchScene& s, int W, int H, int G, int rmax,
+                                const void* rows_all, const void* ent_all,
+                                const long long* offs, int maxrec, const ParityWork& w,
+                                void* cin_ret, hipStream_t stream, const hipEvent_t* ev) {
+  if (G < 1 || G > kMaxShards) return hipErrorInvalidValue;
+  const Scene sc = make_scene(s);
+  ShardOffs o{};
+  for (int g = 0; g < G; ++g) o.off[g] = offs[g];
+  const RowShard* rs = (const RowShard*)rows_all;
+  (void)hipMemsetAsync(w.counters, 0, 16 * sizeof(int), stream);
+  (void)hipMemsetAsync(w.team, 0, sizeof(TeamState), stream);
+  hipLaunchKernelGGL(k_shard_rows, dim3((H + 255) / 256), dim3(256), 0, stream, rs, G, rmax, H,
+                     (RowStats*)w.row_stats);
+  hipLaunchKernelGGL(k_row_scan, dim3(1), dim3(1024), 0, stream, H, (const RowStats*)w.row_stats,
+                     w.row_off, w.row_soff, w.row_prevw, w.row_prevd, w.counters);
+  const int row_blocks = (H + kRowWaves - 1) / kRowWaves;
+  hipLaunchKernelGGL(k_shard_unpack, dim3(row_blocks), dim3(256), 0, stream, rs,
+                     (const ShardEntry*)ent_all, o, G, rmax, W, H, w.row_off, w.row_soff,
+                     w.row_prevw, w.row_prevd, (DepRec*)w.deprec, w.dep_pix, w.seg_start,
+                     w.seg_key, w.wcarry);
+  hipLaunchKernelGGL(k_seg_order, dim3(1), dim3(1024), 0, stream, w.seg_start, w.counters,
+                     w.seg_order, w.batch_state);
+  if (ev) (void)hipEventRecord(ev[0], stream);
+  auto kres = s.n <= kLdsShapes ? k_resolve<true> : k_resolve<false>;
+  hipLaunchKernelGGL(kres, dim3(w.resolve_blocks), dim3(kResolveBlock), w.resolve_lds, stream,
+                     sc, maxrec, (const DepRec*)w.deprec, w.dep_pix, w.seg_key, w.wcarry,
+                     w.seg_start, w.seg_order, w.counters, w.counters + 1, (CinG*)w.cin,
+                     w.team_blocks, w.long_len, (TeamState*)w.team, w.trace, w.coop_group,
+                     w.wave_k, w.resolve_k, w.epoch, w.helpers, w.hand_run);
+  if (ev) (void)hipEventRecord(ev[1], stream);
+  hipLaunchKernelGGL(k_shard_cin, dim3(row_blocks), dim3(256), 0, stream, rs, o, G, rmax, H,
+                     w.row_off, (const CinG*)w.cin, (CinG*)cin_ret);
+  return hipGetLastError();
+}
+
+hipError_t launch_shard_phase_c(const LaunchScene& s, int W, int H, int row0, int row_step,
+                                int maxrec, uint8_t* out, const ParityWork& w, unsigned tag,
+                                unsigned long long* zcount, hipStream_t stream) {
+  const Scene sc = make_scene(s);
+  const Cam cam = make_cam(s, W, H);
+  hipLaunchKernelGGL(stage_fits(s) ? k_dep_chunks<true> : k_dep_chunks<false>,
+                     dim3(w.phase_c_blocks), dim3(kBlock), 0, stream, sc, cam, W, row0, row_step,
+                     maxrec, w.dep_pix, (const DepRec*)w.deprec, (const float4*)w.wcarry,
+                     (CinG*)w.cin, w.counters, out, (uint32_t*)nullptr, zcount,
+                     (TeamState*)w.team, tag);
+  return hipGetLastError();
+}
+
+hipError_t launch_deinterleave(const uint8_t* gathered, int G, int rmax, int W, int H,
+                               uint8_t* img, hipStream_t stream) {
+  if (H <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_deinterleave, dim3(H), dim3(256), 0, stream, gathered, G, rmax, W, H, img);
+  return hipGetLastError();
 }
 
 size_t deprec_bytes() { return sizeof(DepRec); }

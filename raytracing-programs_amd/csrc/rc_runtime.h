@@ -1,0 +1,151 @@
+// rc_runtime.h — internal host-runtime state of libraycast_hip.so shared by rc_api.hip (one
+// device: rc_render, frames in flight) and rc_shard.hip (row shards over several devices).
+// Not part of the C-ABI (include/raycast_hip.h).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <mutex>
+
+#include "raycast_hip.h"
+#include "rc_kernels.h"
+#include "rc_scene.h"
+
+namespace rcrt {
+
+#define HIP_TRY(expr)                                                                   \
+  do {                                                                                  \
+    hipError_t e_ = (expr);                                                             \
+    if (e_ != hipSuccess) {                                                             \
+      std::fprintf(stderr, "Error: HIP call failed: %s (%s) at %s:%d\n", #expr,        \
+                   hipGetErrorString(e_), __FILE__, __LINE__);                          \
+      return -1;                                                                        \
+    }                                                                                   \
+  } while (0)
+
+constexpr int kMaxDevices = 16;
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  int ensure(size_t need) {
+    if (need <= bytes) return 0;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+    if (hipMalloc(&p, need) != hipSuccess) return -1;
+    bytes = need;
+    return 0;
+  }
+};
+
+// One frame's device state: the uploaded scene, the zero-normalize counter and the parity
+// workspace.  The plain path has one (DevCtx::fb); pipelined frames alternate two (Pipe).
+struct FrameBufs {
+  unsigned epoch = 0;   // carry-in tag of the last parity frame in this workspace
+  DevBuf zcount;        // zero-normalize counter
+  DevBuf scene;         // uploaded packed scene
+  const void* scene_src = nullptr;   // host image last uploaded
+  DevBuf cls, wcarry, deprec, rows, dep_pix, seg_key, seg_start, seg_order, batch_state, cin,
+      counters, team, trace;
+};
+
+// Pipelined parity frames (rc_frame_submit).  The device's CUs are split in two partitions
+// (hipExtStreamCreateWithCUMask).  Partition A runs the carry resolvers: kLanes resolver
+// streams, each resolver grid sized to A/kLanes CUs (one workgroup per CU), so the resolvers in
+// flight are always wholly resident side by side (a team spins on co-resident workgroups;
+// at most kLanes resolvers are in flight since each stream runs its resolvers in order).
+// Partition B runs the pixel phases: the frames' phase A one at a time in submission order
+// (each waits for the previous frame's, adone), so the frame whose resolver comes next always
+// has the whole partition; two streams (pix[0], pix[1]) alternate so a frame's compaction —
+// a chain of small latency-bound kernels — overlaps the next frame's phase A; each lane's
+// phase C runs on a stream of its own (pc[lane], after the frame's resolver); a slot's next
+// phase A waits for the slot's previous phase C (cdone).  A resolver is
+// latency-bound (its carry chains), so overlapping kLanes of them multiplies the frame rate
+// until partition B's pixel work becomes the bound.  (RC_PIPE_SLOTSTREAMS: the earlier form,
+// one stream per slot running A, compaction and C in turn.)
+struct Pipe {
+  static constexpr int kSlots = 8;   // frame workspaces (a frame re-uses slot k after k's end)
+  static constexpr int kLanes = 4;   // resolvers in flight (at most)
+  bool init = false;
+  int res_cus = 0;                   // CUs in partition A
+  int lanes = 2;                     // resolver streams in use (RC_PIPE_RESOLVERS)
+  int slots = 4;                     // workspaces / pixel streams in use (RC_PIPE_SLOTS)
+  hipStream_t pix[kSlots] = {}, res[kLanes] = {};
+  hipEvent_t ready[kSlots] = {}, done[kSlots] = {};
+  bool fifo = true;                  // pa = pix[0] + pc[] (false: RC_PIPE_SLOTSTREAMS)
+  hipStream_t pc[kLanes] = {};
+  hipEvent_t cdone[kSlots] = {};
+  bool cpend[kSlots] = {};           // slot k's phase C is enqueued and not yet synchronised
+  hipEvent_t adone[kSlots] = {};     // after slot k's phase A
+  static constexpr int kEv = 64;     // resolver timing events of the last kEv frames
+  hipEvent_t rt[kEv][2] = {};
+  FrameBufs fb[kSlots];
+  long long submitted = 0;           // parity frames since the last rc_frames_wait
+  long long frames = 0;              // frames of any mode since the last rc_frames_wait
+  long long total = 0;               // parity frames ever (slot / stream rotation)
+  long long last = -1;               // slot of the last parity frame
+  bool used[kSlots] = {};
+  bool rt_on = true;                 // resolver timing events recorded (RC_PIPE_NO_RT: off)
+};
+
+struct DevCtx {
+  bool init = false;
+  int device = 0;
+  hipStream_t side = nullptr;   // phase C's side stream
+  hipEvent_t fork = nullptr, join = nullptr;
+  int side_blocks = 0, side_lds = 0;
+  int cus = 256;
+  hipStream_t stream = nullptr;
+  // event sets: [0] start, then per phase ends (fast: [1] = render; parity: [1] phase A,
+  // [2] compaction, [3] resolver, [4] phase C).  Set 0 serves plain calls; inside an
+  // rc_profile_begin/end window every call takes the next set of the pool.
+  static constexpr int kEvSets = 64;
+  hipEvent_t ev[kEvSets][5] = {};
+  int prof_active = 0, prof_calls = 0, prof_parity = 0;
+  DevBuf out;          // rc_render output pixmap
+  uint8_t* stage[2] = {nullptr, nullptr};   // pinned bounce buffers of copy_to_host
+  hipEvent_t stage_ev[2] = {nullptr, nullptr};
+  FrameBufs fb;        // scene, counter and parity workspace of the plain path
+  Pipe pipe;
+  int resident_blocks = 0;
+  int resident_lds = -1;
+  static constexpr int kResCache = 4;   // resident resolver grids per LDS reservation
+  int res_lds[kResCache] = {};
+  int res_blocks[kResCache] = {};
+  size_t parity_pixels = 0;
+  int parity_rows = 0;
+  // rc_render's overlapped copy (parity): the framebuffer leaves on `d2h` while the resolver
+  // runs, then only the DEP entries' colours (`patch`, packed RGB per entry) follow
+  hipStream_t d2h = nullptr;
+  DevBuf patch;
+  uint8_t* pin_pix = nullptr;     // pinned: DEP pixel indices (int64 per entry)
+  uint8_t* pin_patch = nullptr;   // pinned: DEP entries' packed RGB
+  size_t pin_bytes = 0;           // capacity of each pinned buffer, in entries
+  int* pin_cnt = nullptr;         // pinned: counters[0..3]
+  // One render at a time per device: the workspace, TeamState, events and streams above are
+  // shared by every call on this device (rc_render, rc_render_device, rc_frame_submit).
+  std::mutex mu;
+};
+
+extern DevCtx g_ctx[kMaxDevices];
+
+int ctx_get(int device, DevCtx** out);
+int copy_to_host(DevCtx& c, uint8_t* host, const uint8_t* dev, size_t bytes, hipStream_t st);
+void prefault(uint8_t* p, size_t n);
+int upload_scene(FrameBufs& b, hipStream_t stream, const rc_scene* s, rc::LaunchScene& ls);
+int ensure_parity(DevCtx& c, FrameBufs& b, int W, int H, rc::ParityWork& w, int res_cus);
+int report_spin_error(const FrameBufs& b, const char* where);
+double event_ms(hipEvent_t a, hipEvent_t b);
+// rc_shard.hip: rc_render's multi-GPU path (a cached in-process group over devices
+// first..first+n-1); *d_image = the root's de-interleaved image.  The caller holds no lock.
+int render_local_group(int first, int n, const rc_scene* s, int W, int H, const rc_options* opt,
+                       uint8_t** d_image, rc_timing* timing);
+
+}  // namespace rcrt
+
+// the packed scene behind the opaque rc_scene handle
+struct rc_scene {
+  rc_packed_header* img;   // host packed image
+};

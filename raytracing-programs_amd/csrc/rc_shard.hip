@@ -1,0 +1,583 @@
+// rc_shard.hip — row-sharded rendering over several GPUs (C/raycast.c:113-129 is
+// the scan loop whose rows are dealt out).
+//
+// Rows are dealt cyclically: row y -> rank y % G (contiguous blocks are 1.7-2.1x imbalanced at
+// 8 ranks).  A rank renders its rows into a compact local framebuffer (local row
+// j = image row rank + j*G); the root (rank 0) gathers the row blocks over RCCL (ncclGather,
+// xGMI) and undoes the interleave on the device (k_deinterleave).
+//
+// Parity mode adds the carry chain's exchange (C/raycast.c:340 scan-order carry): every rank
+// runs phase A on its rows and packs its DEP entries (record + in-row writer key and carry) and
+// per-row summaries; the root gathers them (ncclGather of the row summaries, ncclSend/ncclRecv
+// of the variable-length entry lists), rebuilds the image's scan order, runs the carry
+// resolver and returns each rank its entries' carry-ins (ncclSend/ncclRecv); every rank then
+// runs phase C on its rows and the framebuffers are gathered as in fast mode.  The resolver
+// stays serial on the root, so parity scaling is capped by it.
+//
+// A group is either one rank of a multi-process job (one process per GPU, rc_group_create_rank,
+// the ncclUniqueId shared by the caller) or every rank in this process (rc_group_create_local:
+// one host thread drives all ranks' streams; RCCL communicators from ncclCommInitAll, or — when
+// ranks share a device, which RCCL does not allow — device copies between the ranks' buffers).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <set>
+#include <vector>
+
+#include "raycast_hip.h"
+#include "rc_kernels.h"
+#include "rc_runtime.h"
+
+using namespace rcrt;
+
+namespace {
+
+#define NCCL_TRY(expr)                                                                   \
+  do {                                                                                   \
+    ncclResult_t r_ = (expr);                                                            \
+    if (r_ != ncclSuccess) {                                                             \
+      std::fprintf(stderr, "Error: RCCL call failed: %s (%s) at %s:%d\n", #expr,        \
+                   ncclGetErrorString(r_), __FILE__, __LINE__);                          \
+      return -1;                                                                         \
+    }                                                                                    \
+  } while (0)
+
+// One rank driven by this process.
+struct Rank {
+  int rank = 0;
+  int device = 0;
+  DevCtx* c = nullptr;
+  hipStream_t stream = nullptr;
+  ncclComm_t comm = nullptr;
+  hipEvent_t ready = nullptr;   // COPY transport: this rank's send buffers are complete
+  FrameBufs fb;                 // rank-local phase A / phase C workspace
+  DevBuf frame;                 // local framebuffer, rmax rows
+  DevBuf ent, rows;             // wire: DEP entries, row summaries
+  DevBuf small;                 // [0] int: DEP entries; [2..3] u64: zero-normalize events
+  int* h_small = nullptr;       // pinned copy of `small`
+  int nrows = 0;
+  long long ndep = 0;
+  // root only
+  FrameBufs rootfb;             // image-wide resolver workspace
+  DevBuf rows_all, ent_all, cin_ret, frames_all, small_all, image;
+  int* h_small_all = nullptr;   // pinned, kMaxShards x 4 ints
+  hipEvent_t ev[6] = {};        // root timeline: start, phase A, resolver start/end, phase C, image
+};
+
+}  // namespace
+
+struct rc_group {
+  int nranks = 1;
+  int transport = RC_XFER_RCCL;
+  std::vector<std::unique_ptr<Rank>> ranks;   // the ranks this process drives
+  Rank* root = nullptr;                       // rank 0 when this process drives it
+  unsigned epoch = 0;                         // carry-in tag of the last sharded parity frame
+  rc_shard_stats last{};
+};
+
+namespace {
+
+int init_rank(Rank& r, int rank, int device) {
+  r.rank = rank;
+  r.device = device;
+  HIP_TRY(hipSetDevice(device));
+  if (ctx_get(device, &r.c)) return -1;
+  HIP_TRY(hipStreamCreateWithFlags(&r.stream, hipStreamNonBlocking));
+  HIP_TRY(hipEventCreateWithFlags(&r.ready, hipEventDisableTiming));
+  HIP_TRY(hipHostMalloc((void**)&r.h_small, 64, hipHostMallocDefault));
+  if (r.small.ensure(64) || r.fb.zcount.ensure(64)) return -1;
+  if (rank == 0) {
+    for (auto& e : r.ev) HIP_TRY(hipEventCreate(&e));
+    HIP_TRY(hipHostMalloc((void**)&r.h_small_all, rc::kMaxShards * 16, hipHostMallocDefault));
+  }
+  return 0;
+}
+
+void free_buf(DevBuf& b) {
+  if (b.p) (void)hipFree(b.p);
+  b.p = nullptr;
+  b.bytes = 0;
+}
+
+void free_frame(FrameBufs& f) {
+  for (DevBuf* b : {&f.zcount, &f.scene, &f.cls, &f.wcarry, &f.deprec, &f.rows, &f.dep_pix,
+                    &f.seg_key, &f.seg_start, &f.seg_order, &f.batch_state, &f.cin, &f.counters,
+                    &f.team, &f.trace})
+    free_buf(*b);
+}
+
+void release_rank(Rank& r) {
+  (void)hipSetDevice(r.device);
+  if (r.stream) (void)hipStreamSynchronize(r.stream);
+  if (r.comm) (void)ncclCommDestroy(r.comm);
+  r.comm = nullptr;
+  free_frame(r.fb);
+  free_frame(r.rootfb);
+  for (DevBuf* b : {&r.frame, &r.ent, &r.rows, &r.small, &r.rows_all, &r.ent_all, &r.cin_ret,
+                    &r.frames_all, &r.small_all, &r.image})
+    free_buf(*b);
+  if (r.h_small) (void)hipHostFree(r.h_small);
+  if (r.h_small_all) (void)hipHostFree(r.h_small_all);
+  r.h_small = r.h_small_all = nullptr;
+  for (auto& e : r.ev)
+    if (e) (void)hipEventDestroy(e);
+  if (r.ready) (void)hipEventDestroy(r.ready);
+  if (r.stream) (void)hipStreamDestroy(r.stream);
+  r.stream = nullptr;
+}
+
+// ------------------------------------------------------------------ transports --
+// Every primitive is issued for all ranks this process drives, inside one RCCL group (a
+// process that drives several devices must group its calls), or as device copies.
+
+// root.recv[r * bytes ..] <- rank r's send (every rank sends `bytes`)
+int gather_fixed(rc_group& g, const std::vector<const void*>& send, void* recv, size_t bytes) {
+  if (g.transport == RC_XFER_RCCL) {
+    NCCL_TRY(ncclGroupStart());
+    for (size_t i = 0; i < g.ranks.size(); ++i) {
+      Rank& r = *g.ranks[i];
+      NCCL_TRY(ncclGather(send[i], r.rank == 0 ? recv : nullptr, bytes, ncclUint8, 0, r.comm,
+                          r.stream));
+    }
+    NCCL_TRY(ncclGroupEnd());
+    return 0;
+  }
+  Rank& root = *g.root;
+  for (size_t i = 0; i < g.ranks.size(); ++i) {
+    Rank& r = *g.ranks[i];
+    HIP_TRY(hipSetDevice(r.device));
+    HIP_TRY(hipEventRecord(r.ready, r.stream));
+  }
+  HIP_TRY(hipSetDevice(root.device));
+  for (size_t i = 0; i < g.ranks.size(); ++i) {
+    Rank& r = *g.ranks[i];
+    if (&r != &root) HIP_TRY(hipStreamWaitEvent(root.stream, r.ready, 0));
+    HIP_TRY(hipMemcpyAsync((char*)recv + (size_t)r.rank * bytes, send[i], bytes, hipMemcpyDefault,
+                           root.stream));
+  }
+  return 0;
+}
+
+// root.recv[off[r] ..] <- rank r's send (bytes[r] bytes; the root knows every rank's size, a
+// rank its own)
+int gather_var(rc_group& g, const std::vector<const void*>& send, void* recv,
+               const std::vector<size_t>& off, const std::vector<size_t>& bytes) {
+  if (g.transport == RC_XFER_RCCL) {
+    NCCL_TRY(ncclGroupStart());
+    for (size_t i = 0; i < g.ranks.size(); ++i) {
+      Rank& r = *g.ranks[i];
+      if (r.rank != 0) {
+        if (bytes[r.rank]) NCCL_TRY(ncclSend(send[i], bytes[r.rank], ncclUint8, 0, r.comm, r.stream));
+        continue;
+      }
+      for (int q = 1; q < g.nranks; ++q)
+        if (bytes[q])
+          NCCL_TRY(ncclRecv((char*)recv + off[q], bytes[q], ncclUint8, q, r.comm, r.stream));
+    }
+    NCCL_TRY(ncclGroupEnd());
+    if (g.root && bytes[0]) {   // the root's own part
+      HIP_TRY(hipSetDevice(g.root->device));
+      HIP_TRY(hipMemcpyAsync(recv, send[0], bytes[0], hipMemcpyDeviceToDevice, g.root->stream));
+    }
+    return 0;
+  }
+  Rank& root = *g.root;
+  for (size_t i = 0; i < g.ranks.size(); ++i) {
+    Rank& r = *g.ranks[i];
+    HIP_TRY(hipSetDevice(r.device));
+    HIP_TRY(hipEventRecord(r.ready, r.stream));
+  }
+  HIP_TRY(hipSetDevice(root.device));
+  for (size_t i = 0; i < g.ranks.size(); ++i) {
+    Rank& r = *g.ranks[i];
+    if (&r != &root) HIP_TRY(hipStreamWaitEvent(root.stream, r.ready, 0));
+    if (bytes[r.rank])
+      HIP_TRY(hipMemcpyAsync((char*)recv + off[r.rank], send[i], bytes[r.rank], hipMemcpyDefault,
+                             root.stream));
+  }
+  return 0;
+}
+
+// rank r's recv <- root.send[off[r] ..] (bytes[r] bytes)
+int scatter_var(rc_group& g, const void* send, const std::vector<void*>& recv,
+                const std::vector<size_t>& off, const std::vector<size_t>& bytes) {
+  if (g.transport == RC_XFER_RCCL) {
+    NCCL_TRY(ncclGroupStart());
+    for (size_t i = 0; i < g.ranks.size(); ++i) {
+      Rank& r = *g.ranks[i];
+      if (r.rank != 0) {
+        if (bytes[r.rank]) NCCL_TRY(ncclRecv(recv[i], bytes[r.rank], ncclUint8, 0, r.comm, r.stream));
+        continue;
+      }
+      for (int q = 1; q < g.nranks; ++q)
+        if (bytes[q])
+          NCCL_TRY(ncclSend((const char*)send + off[q], bytes[q], ncclUint8, q, r.comm, r.stream));
+    }
+    NCCL_TRY(ncclGroupEnd());
+    if (g.root && bytes[0]) {
+      HIP_TRY(hipSetDevice(g.root->device));
+      HIP_TRY(hipMemcpyAsync(recv[0], send, bytes[0], hipMemcpyDeviceToDevice, g.root->stream));
+    }
+    return 0;
+  }
+  Rank& root = *g.root;
+  HIP_TRY(hipSetDevice(root.device));
+  HIP_TRY(hipEventRecord(root.ready, root.stream));
+  for (size_t i = 0; i < g.ranks.size(); ++i) {
+    Rank& r = *g.ranks[i];
+    HIP_TRY(hipSetDevice(r.device));
+    if (&r != &root) HIP_TRY(hipStreamWaitEvent(r.stream, root.ready, 0));
+    if (bytes[r.rank])
+      HIP_TRY(hipMemcpyAsync(recv[i], (const char*)send + off[r.rank], bytes[r.rank],
+                             hipMemcpyDefault, r.stream));
+  }
+  return 0;
+}
+
+int sync_all(rc_group& g) {
+  for (auto& rp : g.ranks) {
+    HIP_TRY(hipSetDevice(rp->device));
+    HIP_TRY(hipStreamSynchronize(rp->stream));
+  }
+  return 0;
+}
+
+double ms_since(std::chrono::steady_clock::time_point t0) {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
+// The whole sharded render; the caller holds every driven device's lock.
+int render_sharded(rc_group& g, const rc_scene* s, int W, int H, const rc_options* opt,
+                   uint8_t* d_image, rc_timing* timing) {
+  const auto t0 = std::chrono::steady_clock::now();
+  const int G = g.nranks;
+  const int rmax = (H + G - 1) / G;
+  const int maxrec = opt->max_recursion;
+  const bool parity = opt->mode == RC_MODE_PARITY && maxrec > 1;
+  const size_t row_bytes = (size_t)W * 3;
+  const size_t block_bytes = (size_t)rmax * row_bytes;
+  Rank* root = g.root;
+  if (root) {
+    HIP_TRY(hipSetDevice(root->device));
+    if (!d_image) {
+      if (root->image.ensure((size_t)H * row_bytes)) return -1;
+      d_image = (uint8_t*)root->image.p;
+    }
+    if (root->frames_all.ensure((size_t)G * block_bytes) || root->small_all.ensure((size_t)G * 16))
+      return -1;
+    HIP_TRY(hipEventRecord(root->ev[0], root->stream));
+  }
+  std::vector<rc::LaunchScene> ls(g.ranks.size());
+  std::vector<rc::ParityWork> w(g.ranks.size());
+  // 1. every rank: its rows (fast: the whole render; parity: phase A + the wire records)
+  for (size_t i = 0; i < g.ranks.size(); ++i) {
+    Rank& r = *g.ranks[i];
+    HIP_TRY(hipSetDevice(r.device));
+    r.nrows = (H - r.rank + G - 1) / G;
+    if (r.nrows < 0) r.nrows = 0;
+    if (r.frame.ensure(block_bytes)) return -1;
+    if (upload_scene(r.fb, r.stream, s, ls[i])) return -1;
+    unsigned long long* zc = (unsigned long long*)r.fb.zcount.p;
+    HIP_TRY(hipMemsetAsync(zc, 0, sizeof(unsigned long long), r.stream));
+    if (!parity) {
+      if (r.nrows > 0)
+        HIP_TRY(rc::launch_render(ls[i], W, H, r.rank, G, r.nrows, maxrec, (uint8_t*)r.frame.p,
+                                  zc, r.stream));
+      continue;
+    }
+    const int lrows = r.nrows > 0 ? r.nrows : 1;
+    if (ensure_parity(*r.c, r.fb, W, lrows, w[i], r.c->cus) ||
+        r.ent.ensure((size_t)lrows * W * rc::shard_entry_bytes()) ||
+        r.rows.ensure((size_t)rmax * rc::shard_row_bytes())) {
+      std::fprintf(stderr, "Error: out of device memory for the shard workspace\n");
+      return -1;
+    }
+    HIP_TRY(rc::launch_shard_local(ls[i], W, H, r.rank, G, r.nrows, maxrec, (uint8_t*)r.frame.p,
+                                   w[i], r.ent.p, r.rows.p, zc, r.stream));
+    HIP_TRY(hipMemcpyAsync(r.small.p, w[i].counters + 2, sizeof(int), hipMemcpyDeviceToDevice,
+                           r.stream));
+  }
+  if (root) HIP_TRY(hipEventRecord(root->ev[1], root->stream));
+  if (parity) {
+    // 2. row summaries and entry counts to the root
+    std::vector<const void*> sr, sc;
+    for (auto& rp : g.ranks) {
+      sr.push_back(rp->rows.p);
+      sc.push_back(rp->small.p);
+    }
+    if (root && (root->rows_all.ensure((size_t)G * rmax * rc::shard_row_bytes()))) return -1;
+    if (gather_fixed(g, sr, root ? root->rows_all.p : nullptr, (size_t)rmax * rc::shard_row_bytes()) ||
+        gather_fixed(g, sc, root ? root->small_all.p : nullptr, 16))
+      return -1;
+    for (auto& rp : g.ranks) {
+      HIP_TRY(hipSetDevice(rp->device));
+      HIP_TRY(hipMemcpyAsync(rp->h_small, rp->small.p, 16, hipMemcpyDeviceToHost, rp->stream));
+    }
+    if (root)
+      HIP_TRY(hipMemcpyAsync(root->h_small_all, root->small_all.p, (size_t)G * 16,
+                             hipMemcpyDeviceToHost, root->stream));
+    if (sync_all(g)) return -1;
+    std::vector<size_t> cnt(G, 0), off(G, 0), eb(G), eo(G), cb(G), co(G);
+    for (auto& rp : g.ranks) rp->ndep = rp->h_small[0];
+    for (int q = 0; q < G; ++q) cnt[q] = root ? (size_t)root->h_small_all[4 * q] : 0;
+    for (auto& rp : g.ranks) cnt[rp->rank] = (size_t)rp->ndep;
+    size_t total = 0;
+    for (int q = 0; q < G; ++q) {
+      off[q] = total;
+      total += cnt[q];
+    }
+    for (int q = 0; q < G; ++q) {
+      eb[q] = cnt[q] * rc::shard_entry_bytes();
+      eo[q] = off[q] * rc::shard_entry_bytes();
+      cb[q] = cnt[q] * (size_t)rc::kCinBytes;
+      co[q] = off[q] * (size_t)rc::kCinBytes;
+    }
+    // this frame's carry-in tag, the same on every rank (ranks render in lockstep)
+    g.epoch = g.epoch + 1 >= 0x80000000u ? 1 : g.epoch + 1;
+    // 3. the entries to the root, the resolver, the carry-ins back
+    rc::ParityWork wr{};
+    if (root) {
+      HIP_TRY(hipSetDevice(root->device));
+      root->rootfb.epoch = g.epoch - 1;
+      root->rootfb.scene_src = s->img;   // the resolver's evaluator is specialised by shape count
+      if (root->ent_all.ensure(total * rc::shard_entry_bytes() + 64) ||
+          root->cin_ret.ensure(total * (size_t)rc::kCinBytes + 64) ||
+          ensure_parity(*root->c, root->rootfb, W, H, wr, root->c->cus)) {
+        std::fprintf(stderr, "Error: out of device memory for the root's resolver workspace\n");
+        return -1;
+      }
+      if (root->rootfb.epoch != g.epoch) {   // ensure_parity cleared the tags on a wrap
+        g.epoch = root->rootfb.epoch;
+      }
+    }
+    std::vector<const void*> se;
+    for (auto& rp : g.ranks) se.push_back(rp->ent.p);
+    if (gather_var(g, se, root ? root->ent_all.p : nullptr, eo, eb)) return -1;
+    if (root) {
+      HIP_TRY(hipSetDevice(root->device));
+      std::vector<long long> offs(off.begin(), off.end());
+      hipEvent_t rev[2] = {root->ev[2], root->ev[3]};
+      HIP_TRY(rc::launch_shard_resolve(ls[0], W, H, G, rmax, root->rows_all.p, root->ent_all.p,
+                                       offs.data(), maxrec, wr, root->cin_ret.p, root->stream,
+                                       rev));
+    }
+    std::vector<void*> rcv;
+    for (size_t i = 0; i < g.ranks.size(); ++i) rcv.push_back(w[i].cin);
+    if (scatter_var(g, root ? root->cin_ret.p : nullptr, rcv, co, cb)) return -1;
+    // 4. every rank: phase C of its entries
+    for (size_t i = 0; i < g.ranks.size(); ++i) {
+      Rank& r = *g.ranks[i];
+      if (!r.ndep) continue;
+      HIP_TRY(hipSetDevice(r.device));
+      HIP_TRY(rc::launch_shard_phase_c(ls[i], W, H, r.rank, G, maxrec, (uint8_t*)r.frame.p, w[i],
+                                       g.epoch, (unsigned long long*)r.fb.zcount.p, r.stream));
+    }
+  }
+  if (root) HIP_TRY(hipEventRecord(root->ev[4], root->stream));
+  // 5. the row blocks and the event counts to the root, the interleave undone there
+  std::vector<const void*> sf, sz;
+  for (auto& rp : g.ranks) {
+    HIP_TRY(hipSetDevice(rp->device));
+    HIP_TRY(hipMemcpyAsync((char*)rp->small.p + 8, rp->fb.zcount.p, 8, hipMemcpyDeviceToDevice,
+                           rp->stream));
+    sf.push_back(rp->frame.p);
+    sz.push_back(rp->small.p);
+  }
+  if (gather_fixed(g, sf, root ? root->frames_all.p : nullptr, block_bytes) ||
+      gather_fixed(g, sz, root ? root->small_all.p : nullptr, 16))
+    return -1;
+  if (root) {
+    HIP_TRY(hipSetDevice(root->device));
+    HIP_TRY(rc::launch_deinterleave((const uint8_t*)root->frames_all.p, G, rmax, W, H, d_image,
+                                    root->stream));
+    HIP_TRY(hipMemcpyAsync(root->h_small_all, root->small_all.p, (size_t)G * 16,
+                           hipMemcpyDeviceToHost, root->stream));
+    HIP_TRY(hipEventRecord(root->ev[5], root->stream));
+  }
+  if (sync_all(g)) return -1;
+  int rc = 0;
+  if (parity) {
+    for (auto& rp : g.ranks)
+      if (rp->fb.team.p && report_spin_error(rp->fb, "shard phase C")) rc = -1;
+    if (root && report_spin_error(root->rootfb, "shard resolver")) rc = -1;
+  }
+  rc_shard_stats& st = g.last;
+  std::memset(&st, 0, sizeof st);
+  st.total_ms = ms_since(t0);
+  if (root) {
+    st.ranks = G;
+    st.local_ms = event_ms(root->ev[0], root->ev[1]);
+    st.image_ms = event_ms(root->ev[4], root->ev[5]);
+    st.device_ms = event_ms(root->ev[0], root->ev[5]);
+    for (int q = 0; q < G; ++q) {
+      long long z = 0;
+      std::memcpy(&z, root->h_small_all + 4 * q + 2, sizeof z);
+      st.zero_normalize += z;
+    }
+    st.image_bytes = (long long)G * (long long)block_bytes;
+    if (parity) {
+      st.exchange_in_ms = event_ms(root->ev[1], root->ev[2]);
+      st.resolve_ms = event_ms(root->ev[2], root->ev[3]);
+      st.phase_c_ms = event_ms(root->ev[3], root->ev[4]);
+      for (int q = 0; q < G; ++q) st.dep_pixels += root->h_small_all[4 * q];
+      st.entry_bytes = st.dep_pixels * (long long)rc::shard_entry_bytes();
+      st.carry_bytes = st.dep_pixels * (long long)rc::kCinBytes;
+    }
+  }
+  if (timing) {
+    std::memset(timing, 0, sizeof *timing);
+    timing->total_ms = st.total_ms;
+    timing->kernel_ms = st.device_ms;
+    timing->resolve_ms = st.resolve_ms;
+    timing->dep_pixels = st.dep_pixels;
+    timing->zero_normalize = st.zero_normalize;
+  }
+  return rc;
+}
+
+// Lock every driven device (ascending order: no lock-order inversion between groups).
+struct DeviceLocks {
+  std::vector<std::unique_lock<std::mutex>> held;
+  explicit DeviceLocks(rc_group& g) {
+    std::set<int> devs;
+    for (auto& rp : g.ranks) devs.insert(rp->device);
+    for (int d : devs) held.emplace_back(g_ctx[d].mu);
+  }
+};
+
+}  // namespace
+
+namespace rcrt {
+
+// rc_render's multi-GPU path: a cached in-process group over devices first..first+n-1.
+int render_local_group(int first, int n, const rc_scene* s, int W, int H, const rc_options* opt,
+                       uint8_t** d_image, rc_timing* timing) {
+  static std::mutex mu;
+  static rc_group* cached = nullptr;
+  static int c_first = -1, c_n = 0;
+  std::lock_guard<std::mutex> lk(mu);
+  if (!cached || c_first != first || c_n != n) {
+    if (cached) rc_group_destroy(cached);
+    std::vector<int> devs(n);
+    for (int i = 0; i < n; ++i) devs[i] = first + i;
+    cached = rc_group_create_local(n, devs.data(), RC_XFER_AUTO);
+    if (!cached) return -1;
+    c_first = first;
+    c_n = n;
+  }
+  DeviceLocks locks(*cached);
+  if (render_sharded(*cached, s, W, H, opt, nullptr, timing)) return -1;
+  *d_image = (uint8_t*)cached->root->image.p;
+  return 0;
+}
+
+}  // namespace rcrt
+
+extern "C" {
+
+int rc_group_unique_id(unsigned char id[RC_GROUP_ID_BYTES]) {
+  static_assert(sizeof(ncclUniqueId) == RC_GROUP_ID_BYTES, "ncclUniqueId size");
+  ncclUniqueId u;
+  NCCL_TRY(ncclGetUniqueId(&u));
+  std::memcpy(id, &u, sizeof u);
+  return 0;
+}
+
+rc_group* rc_group_create_rank(int nranks, int rank, const unsigned char id[RC_GROUP_ID_BYTES],
+                               int device) {
+  if (nranks < 1 || nranks > rc::kMaxShards || rank < 0 || rank >= nranks || !id) return nullptr;
+  auto g = std::make_unique<rc_group>();
+  g->nranks = nranks;
+  g->transport = RC_XFER_RCCL;
+  auto r = std::make_unique<Rank>();
+  if (init_rank(*r, rank, device)) return nullptr;
+  ncclUniqueId u;
+  std::memcpy(&u, id, sizeof u);
+  if (ncclCommInitRank(&r->comm, nranks, u, rank) != ncclSuccess) {
+    std::fprintf(stderr, "Error: ncclCommInitRank failed (rank %d of %d)\n", rank, nranks);
+    release_rank(*r);
+    return nullptr;
+  }
+  if (rank == 0) g->root = r.get();
+  g->ranks.push_back(std::move(r));
+  return g.release();
+}
+
+rc_group* rc_group_create_local(int nranks, const int* devices, int transport) {
+  if (nranks < 1 || nranks > rc::kMaxShards || !devices) return nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess) return nullptr;
+  std::set<int> distinct;
+  for (int i = 0; i < nranks; ++i) {
+    if (devices[i] < 0 || devices[i] >= ndev) {
+      std::fprintf(stderr, "Error: device %d not available (%d devices)\n", devices[i], ndev);
+      return nullptr;
+    }
+    distinct.insert(devices[i]);
+  }
+  if (transport == RC_XFER_AUTO)
+    transport = (int)distinct.size() == nranks ? RC_XFER_RCCL : RC_XFER_COPY;
+  if (transport == RC_XFER_RCCL && (int)distinct.size() != nranks) {
+    std::fprintf(stderr, "Error: RCCL ranks need distinct devices (use RC_XFER_COPY)\n");
+    return nullptr;
+  }
+  auto g = std::make_unique<rc_group>();
+  g->nranks = nranks;
+  g->transport = transport;
+  for (int i = 0; i < nranks; ++i) {
+    auto r = std::make_unique<Rank>();
+    if (init_rank(*r, i, devices[i])) return nullptr;
+    g->ranks.push_back(std::move(r));
+  }
+  g->root = g->ranks[0].get();
+  if (transport == RC_XFER_RCCL) {
+    std::vector<ncclComm_t> comms(nranks);
+    if (ncclCommInitAll(comms.data(), nranks, devices) != ncclSuccess) {
+      std::fprintf(stderr, "Error: ncclCommInitAll failed (%d devices)\n", nranks);
+      for (auto& rp : g->ranks) release_rank(*rp);
+      return nullptr;
+    }
+    for (int i = 0; i < nranks; ++i) g->ranks[i]->comm = comms[i];
+  }
+  return g.release();
+}
+
+void rc_group_destroy(rc_group* g) {
+  if (!g) return;
+  for (auto& rp : g->ranks) release_rank(*rp);
+  delete g;
+}
+
+int rc_group_size(const rc_group* g) { return g ? g->nranks : 0; }
+
+int rc_group_transport(const rc_group* g) { return g ? g->transport : -1; }
+
+int rc_render_sharded(rc_group* g, const rc_scene* s, int W, int H, const rc_options* opt,
+                      uint8_t* d_image, rc_timing* timing) {
+  if (!g || !s || !opt || W <= 0 || H <= 0) return -1;
+  if ((long long)W * H >= (1ll << 31)) return -1;   // DEP indices and wire pixels are 32-bit
+  int dev = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  int rc;
+  {
+    DeviceLocks locks(*g);
+    rc = render_sharded(*g, s, W, H, opt, d_image, timing);
+  }
+  (void)hipSetDevice(dev);
+  return rc;
+}
+
+int rc_group_last_stats(const rc_group* g, rc_shard_stats* out) {
+  if (!g || !out) return -1;
+  *out = g->last;
+  return 0;
+}
+
+}  // extern "C"

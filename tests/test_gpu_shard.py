@@ -1,0 +1,134 @@
+"""GPU tests of the row-sharded path (rc_group / rc_render_sharded) through the
+C-ABI: rows dealt cyclically over G ranks, the root gathers the row blocks; in parity mode the
+root also gathers every rank's DEP entries, resolves the scan-order carry chain and returns the
+carry-ins for phase C on the ranks.  Every image must be byte-identical to the reference's
+(golden md5) or to the CPU oracle.
+
+The box has one GPU, so G > 1 runs as G ranks on device 0 with device copies between their
+buffers (RC_XFER_COPY: the same kernels, wire records and exchange order as RCCL); the RCCL
+transport itself runs with one rank (ncclGather / group calls with a single communicator),
+both from one process (ncclCommInitAll) and as a rank of a multi-process job
+(ncclCommInitRank)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from helpers import GOLDEN, golden_key, golden_table, oracle_render, p3_md5, rc, scene_path
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+SMALL = ["simple", "reflection", "quadric", "example2", "example3", "quadric2"]
+
+
+@pytest.fixture(scope="module")
+def table():
+    return golden_table()
+
+
+@pytest.fixture(scope="module")
+def scenes():
+    return {n: rc.Scene.from_file(scene_path(n)) for n in SMALL + ["phantom_four", "phantom_two"]}
+
+
+_groups = {}
+
+
+def group(devices, transport):
+    key = (tuple(devices), transport)
+    if key not in _groups:
+        _groups[key] = rc.Group.local(devices, transport)
+    return _groups[key]
+
+
+def sharded(g, scene, w, h, depth, mode, timing=None):
+    out = torch.empty((h, w, 3), dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    g.render(scene, w, h, out.data_ptr(), depth=depth, mode=mode, timing=timing)
+    return out.cpu().numpy()
+
+
+@pytest.mark.parametrize("G", [1, 2, 3, 8])
+@pytest.mark.parametrize("mode", ["parity", "fast"])
+def test_sharded_small_goldens(G, mode, scenes, table):
+    g = group([0] * G, "copy")
+    assert g.size == G and g.transport == "copy"
+    for name in SMALL:
+        for d in (0, 4, 6):
+            img = sharded(g, scenes[name], 256, 256, d, mode)
+            key = golden_key(name, 256, 256, d, mode)
+            assert p3_md5(img) == table[key]["md5"], f"{key} G={G}"
+
+
+@pytest.mark.parametrize("key", ["quadric:4096x4096:d6:parity", "quadric:4096x4096:d6:fast",
+                                 "reflection:2048x2048:d4:parity", "simple:1024x1024:d0:parity",
+                                 "quadric:333x517:d6:parity", "quadric:1x4096:d6:parity"])
+@pytest.mark.parametrize("G", [2, 8])
+def test_sharded_configs(key, G, scenes, table):
+    name, size, d, mode = key.split(":")
+    w, h = map(int, size.split("x"))
+    t = {}
+    img = sharded(group([0] * G, "copy"), scenes[name], w, h, int(d[1:]), mode, t)
+    assert p3_md5(img) == table[key]["md5"], f"{key} G={G}"
+    if mode == "parity" and int(d[1:]) > 0:
+        assert t["dep_pixels"] == table[key].get("dep_pixels", t["dep_pixels"])
+
+
+def test_sharded_ragged_vs_oracle(scenes):
+    """Images with fewer rows than ranks, single columns and odd sizes, against the oracle."""
+    g5 = group([0] * 5, "copy")
+    for name, w, h, d in [("quadric", 37, 29, 6), ("quadric", 50, 2, 6), ("reflection", 1, 41, 4),
+                          ("simple", 3, 1, 6), ("quadric2", 64, 63, 6)]:
+        for mode in ("parity", "fast"):
+            want, st = oracle_render(scenes[name], w, h, d, mode)
+            t = {}
+            got = sharded(g5, scenes[name], w, h, d, mode, t)
+            np.testing.assert_array_equal(got, want, err_msg=f"{name} {w}x{h} d{d} {mode}")
+            assert t["zero_normalize"] == st["zero_normalize"]
+            if mode == "parity" and d > 0:
+                assert t["dep_pixels"] == st["dep_pixels"]
+
+
+def test_sharded_phantom_lit(scenes):
+    """Lit phantom (dep_fast off: phase C recomputes the whole pixel on its rank, from the
+    image row of the rank-local pixel) against the reference's md5s."""
+    tab = json.load(open(os.path.join(GOLDEN, "phantom_md5.json")))
+    g3 = group([0] * 3, "copy")
+    for key, want in sorted(tab.items()):
+        name, size, d, mode = key.split(":")
+        w, h = map(int, size.split("x"))
+        assert p3_md5(sharded(g3, scenes[name], w, h, int(d[1:]), mode)) == want["md5"], key
+
+
+@pytest.mark.parametrize("mode", ["parity", "fast"])
+def test_sharded_rccl_one_rank(mode, scenes, table):
+    """The RCCL transport: one communicator from ncclCommInitAll, and one rank of a
+    multi-process job from ncclCommInitRank with a fresh unique id."""
+    key = golden_key("quadric", 256, 256, 6, mode)
+    g = group([0], "rccl")
+    assert g.transport == "rccl"
+    assert p3_md5(sharded(g, scenes["quadric"], 256, 256, 6, mode)) == table[key]["md5"]
+    gr = rc.Group.rank(1, 0, rc.Group.unique_id(), 0)
+    try:
+        assert p3_md5(sharded(gr, scenes["quadric"], 256, 256, 6, mode)) == table[key]["md5"]
+        big = "quadric:4096x4096:d6:" + mode
+        assert p3_md5(sharded(gr, scenes["quadric"], 4096, 4096, 6, mode)) == table[big]["md5"]
+        st = gr.stats()
+        assert st["ranks"] == 1 and st["image_bytes"] == 4096 * 4096 * 3
+    finally:
+        gr.close()
+
+
+def test_sharded_repeat_and_stats(scenes, table):
+    """Back-to-back sharded frames reuse every buffer (carry-in tags advance per frame); the
+    exchange volumes follow the wire formats (64 B per DEP entry in, 24 B carry-in back)."""
+    key = "quadric:4096x4096:d6:parity"
+    g4 = group([0] * 4, "copy")
+    for _ in range(3):
+        assert p3_md5(sharded(g4, scenes["quadric"], 4096, 4096, 6, "parity")) == table[key]["md5"]
+    st = g4.stats()
+    assert st["ranks"] == 4 and st["dep_pixels"] == 2804464
+    assert st["entry_bytes"] == 64 * st["dep_pixels"] and st["carry_bytes"] == 24 * st["dep_pixels"]
+    assert st["resolve_ms"] > 0.0 and st["device_ms"] >= st["resolve_ms"]
