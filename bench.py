@@ -14,13 +14,16 @@ Fast mode: one render kernel per frame.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--mode parity|fast] [--inflight 1|2]
 
-Multi-GPU (torchrun, one rank per GPU, RANK/LOCAL_RANK/WORLD_SIZE from the env):
-  parity: the image's scan-order carry chain is one serial dependency,
-          so the path does not shard: every rank renders its own full image (replicas, no
-          data-path collective) and `value` = N images' pixels / max rank time ("weak").
-  fast:   rows dealt cyclically (row r -> rank r mod N), each rank renders its rows, the row
-          blocks are gathered over RCCL (all_gather_into_tensor, "nccl" backend) and
-          de-interleaved on rank 0 inside the timed region ("strong").
+Multi-GPU (torchrun, one rank per GPU, RANK/LOCAL_RANK/WORLD_SIZE from the env): every rank
+joins an rc_group (the library's own RCCL communicator; rank 0's ncclUniqueId shared over
+torch.distributed).
+  fast:   one image row-sharded (row y -> rank y % N), rendered by rc_render_sharded: each
+          rank its rows, ncclGather of the row blocks to rank 0, de-interleaved on its device
+          ("strong").
+  parity: the carry chain's resolver is serial, so the headline is N replicas,
+          one image per GPU, no data-path collective ("weak"); the row-sharded single image
+          (rank 0 gathers the DEP entries, resolves, returns carry-ins) is timed after the
+          timed region and reported as `sharded_single_image` (--shard makes it the step).
 
 Rank 0 prints one JSON line with `roofline` (the dominant kernel, timed live with HIP events
 on its stream through rc_profile_begin/end), per-phase times and `cpu_baseline` (the reference
@@ -37,12 +40,19 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 
 # Algorithmic work: SURVEY.md §8d's per-operation weights (sphere test
-# 29, plane 15, quadric 81, hit post-processing ~26, light setup 18, unshadowed light 70,
-# reflect+normalize 21, ray generation 15) applied to the exact per-pixel work counts of
-# the reference at this config (oracle counters, quadric 4096^2 depth 6).
+# 29, plane 15, quadric 81, hit post-processing 26 per non-shadow nearest, light setup 18 per
+# shadow ray, unshadowed light 70, reflect+normalize 21 per bounce, ray generation 15) applied
+# to the reference's exact per-pixel work counts at each config (CPU oracle counters over the
+# whole image, tests/helpers.oracle_render stats).  A carry transfer function (one DEP entry
+# of the resolver) = (depth - 1) bounce levels x (every shape's test + reflect/normalize) +
+# hit post-processing for its hits (quadric: 5 x (287 + 21) + 3 x 26 = 1618, the creep
+# pattern hit/miss/hit/miss/hit; reflection d4: 3 x (421 + 21) + 2 x 26 = 1378).
 WORK = {
-    "quadric:4096:6": {"render_flop_per_px": 1374.0,   # full render, every pixel
-                       "dep_flop_per_entry": 1618.0},  # one carry transfer function
+    "simple:1024:0": {"render_flop_per_px": 260.1},                 # C2 (no bounce: no DEP)
+    "simple:256:6": {"render_flop_per_px": 406.4, "dep_flop_per_entry": 5 * (102 + 21) + 3 * 26},
+    "reflection:2048:4": {"render_flop_per_px": 930.6, "dep_flop_per_entry": 1378.0},   # C3
+    "quadric:4096:6": {"render_flop_per_px": 1373.9, "dep_flop_per_entry": 1618.0},     # C4
+    "quadric:8192:6": {"render_flop_per_px": 1381.7, "dep_flop_per_entry": 1618.0},     # C5
 }
 PEAK_FP64_TFLOPS = 78.6    # MI355X vector FP64 (MI355X_MICROARCH.md: FP32 157.3 / 2)
 PEAK_HBM_GBS = 8000.0      # MI355X HBM3E
@@ -102,10 +112,22 @@ def end_to_end(pkg, scene, W, H, depth, mode, reps=5):
                     "rc_render's own clock"}
 
 
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
 def cpu_baseline(scene_path, size, depth):
     """The reference itself (oracle/_ref/ref_timer_d<depth>: the C/ sources built like
-    C/Makefile:4, raycast() timed alone) on the same image on one pinned host core; falls
-    back to the CPU restatement (oracle/build) when the reference build is absent."""
+    C/Makefile:4, raycast() timed alone) on the same image on one pinned host core, median of
+    3 runs (1 above 4096^2: ~40 s each); falls back to the CPU restatement
+    (oracle/build) when the reference build is absent."""
     ref = os.path.join(ROOT, "oracle", "_ref", f"ref_timer_d{depth}")
     if os.path.exists(ref):
         cmd, kind = [ref, str(size), str(size), scene_path], "reference"
@@ -113,19 +135,39 @@ def cpu_baseline(scene_path, size, depth):
         cmd = [os.path.join(ROOT, "oracle", "build", "oracle_raytrace"), str(size), str(size),
                scene_path, "/dev/null", str(depth)]
         kind = "port"
+    runs = 3 if size <= 4096 else 1
+    info = {"cpu_model": cpu_model(), "nproc": os.cpu_count()}
     try:
         try:
             core = sorted(os.sched_getaffinity(0))[0]
             cmd = ["taskset", "-c", str(core)] + cmd
         except (AttributeError, OSError):
             pass
-        out = subprocess.run(cmd, capture_output=True, text=True, timeout=300, check=True).stdout
-        r = json.loads([l for l in out.splitlines() if l.startswith("{")][-1])
+        res = []
+        for _ in range(runs):
+            out = subprocess.run(cmd, capture_output=True, text=True, timeout=300,
+                                 check=True).stdout
+            res.append(json.loads([l for l in out.splitlines() if l.startswith("{")][-1]))
+        res.sort(key=lambda r: r["seconds"])
+        r = res[len(res) // 2]
         return {"value": round(r["rays_per_s"], 1), "unit": "rays/s", "cores": 1, "kind": kind,
-                "sample": f"full {size}x{size} quadric.scene depth {depth} render, raycast() "
-                          f"only, 1 pinned core: {r['seconds']:.2f} s"}
+                "sample": f"full {size}x{size} {os.path.basename(scene_path)} depth {depth} "
+                          f"render, raycast() only, 1 pinned core, median of {runs}: "
+                          f"{r['seconds']:.2f} s", **info}
     except Exception as e:  # noqa: BLE001
-        return {"value": None, "unit": "rays/s", "cores": 1, "kind": kind, "sample": f"failed: {e}"}
+        return {"value": None, "unit": "rays/s", "cores": 1, "kind": kind,
+                "sample": f"failed: {e}", **info}
+
+
+def make_group(pkg, dist, world, rank, local):
+    """This rank's rc_group (one process per GPU): rank 0 makes the RCCL unique id, the job
+    shares it over torch.distributed, every rank joins (ncclCommInitRank inside the library)."""
+    import torch
+    uid = torch.zeros(pkg.GROUP_ID_BYTES, dtype=torch.uint8, device="cuda")
+    if rank == 0:
+        uid.copy_(torch.frombuffer(bytearray(pkg.Group.unique_id()), dtype=torch.uint8))
+    dist.broadcast(uid, 0)
+    return pkg.Group.rank(world, rank, bytes(uid.cpu().tolist()), local)
 
 
 def main():
@@ -145,6 +187,9 @@ def main():
     ap.add_argument("--inflight", type=int, default=2, choices=[1, 2],
                     help="parity frames in flight: 2 = rc_frame_submit (the next frame's pixel "
                          "phases beside this frame's resolver), 1 = one rc_render_device per step")
+    ap.add_argument("--shard", action="store_true",
+                    help="N>1 parity: time the row-sharded single image (rc_render_sharded) as "
+                         "the step instead of N replicas")
     args = ap.parse_args()
 
     import torch
@@ -153,11 +198,11 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if os.environ.get("RC_BENCH_BACKEND", "nccl") != "nccl":   # 1-GPU rehearsal: ranks share GPUs
+    backend = os.environ.get("RC_BENCH_BACKEND", "nccl")   # gloo: 1-GPU rehearsal only
+    if backend != "nccl":   # rehearsal: ranks share the GPUs, so no RCCL group (replicas only)
         local %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if world > 1:
-        backend = os.environ.get("RC_BENCH_BACKEND", "nccl")   # gloo: 1-GPU rehearsal only
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
@@ -167,20 +212,26 @@ def main():
     scene = pkg.Scene.from_file(scene_path)
     W = H = args.size
     mode = args.mode
-    sharded = world > 1 and mode == "fast"
-    if sharded:
-        row0, step_rows, nrows = pkg.row_shard(H, rank, world)
-    else:
-        row0, step_rows, nrows = 0, 1, H
-    out = torch.empty((nrows, W, 3), dtype=torch.uint8, device="cuda")
+    parity = mode == "parity" and args.depth > 0
+    group, group_err = None, None
+    if world > 1 and backend == "nccl":
+        try:
+            group = make_group(pkg, dist, world, rank, local)
+        except Exception as e:  # noqa: BLE001 — reported in the line; replicas still run
+            group_err = f"{type(e).__name__}: {e}"
+        ok = torch.tensor([0 if group is None else 1], dtype=torch.int32, device="cuda")
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if int(ok.item()) == 0 and group is not None:   # every rank or none uses the group
+            group.close()
+            group, group_err = None, group_err or "another rank failed to join the rc_group"
+    # the step: fast mode over N GPUs = one image row-sharded (strong); parity over N GPUs =
+    # N replicas, one image per GPU (weak: the carry resolver is serial), or the
+    # sharded single image with --shard
+    sharded = group is not None and (mode == "fast" or args.shard)
+    out = torch.empty((H, W, 3), dtype=torch.uint8, device="cuda")
     stream = torch.cuda.current_stream()
-    if sharded:
-        rows_max = (H + world - 1) // world
-        gathered = torch.empty((world, rows_max, W, 3), dtype=torch.uint8, device="cuda")
-        send = torch.zeros((rows_max, W, 3), dtype=torch.uint8, device="cuda")
-        full = torch.empty((rows_max * world, W, 3), dtype=torch.uint8, device="cuda")
 
-    piped = mode == "parity" and args.depth > 0 and args.inflight == 2 and not sharded
+    piped = parity and args.inflight == 2 and not sharded
     if piped:   # every frame of the timed region gets its own output image
         outs = [torch.empty((H, W, 3), dtype=torch.uint8, device="cuda")
                 for _ in range(max(args.steps, 1))]
@@ -192,13 +243,8 @@ def main():
             buf = outs[frame_no[0] % len(outs)]
             frame_no[0] += 1
             pkg.frame_submit(scene, W, H, buf.data_ptr(), depth=args.depth, mode=mode)
-            return
-        if sharded:
-            pkg.render_device(scene, W, H, send.data_ptr(), stream.cuda_stream, depth=args.depth,
-                              mode=mode, row0=row0, row_step=step_rows, nrows=nrows)
-            pkg.gather_rows(send, gathered, dist)
-            if rank == 0:   # image row y lives on rank y % N at local row y // N
-                full.copy_(pkg.deinterleave(gathered, rows_max * world))
+        elif sharded:   # synchronous: the root holds the de-interleaved image when it returns
+            group.render(scene, W, H, out.data_ptr(), depth=args.depth, mode=mode)
         else:
             pkg.render_device(scene, W, H, out.data_ptr(), stream.cuda_stream, depth=args.depth,
                               mode=mode)
@@ -253,18 +299,46 @@ def main():
     tmax = float(tmax.item())
 
     tim = {}
+    shard_stats = group.stats() if sharded else None
     if piped:
         tim = pipe_tim
+    elif sharded:
+        tim = {"dep_pixels": shard_stats["dep_pixels"], "resolve_ms": shard_stats["resolve_ms"]}
+        phases = {"local_ms": shard_stats["local_ms"],
+                  "exchange_in_ms": shard_stats["exchange_in_ms"],
+                  "resolve_ms": shard_stats["resolve_ms"], "phase_c_ms": shard_stats["phase_c_ms"],
+                  "image_ms": shard_stats["image_ms"], "total_ms": shard_stats["device_ms"],
+                  "render_ms": shard_stats["local_ms"] if not parity else 0.0,
+                  "phase_a_ms": shard_stats["local_ms"] if parity else 0.0}
     elif not args.timed_only:
-        pkg.render_device(scene, W, H, (send if sharded else out).data_ptr(), stream.cuda_stream,
-                          depth=args.depth, mode=mode, row0=row0, row_step=step_rows,
-                          nrows=nrows, timing=tim)
+        pkg.render_device(scene, W, H, out.data_ptr(), stream.cuda_stream, depth=args.depth,
+                          mode=mode, timing=tim)
     torch.cuda.synchronize()
+    # N>1 parity replicas: the sharded single image as well, reported beside (never as) value
+    shard_leg = None
+    if group is not None and not sharded and not args.timed_only:
+        dist.barrier()
+        group.render(scene, W, H, out.data_ptr(), depth=args.depth, mode=mode)   # warm
+        dist.barrier()
+        ts = time.perf_counter()
+        reps = 5
+        for _ in range(reps):
+            group.render(scene, W, H, out.data_ptr(), depth=args.depth, mode=mode)
+        dist.barrier()
+        ms = (time.perf_counter() - ts) * 1e3 / reps
+        st = group.stats()
+        shard_leg = {"value": round(W * H / (ms * 1e-3), 1), "unit": "rays/s", "ms": round(ms, 4),
+                     "note": f"one {W}x{H} image row-sharded over {world} GPUs (rc_render_sharded: "
+                             "phase A on every rank, DEP entries gathered to rank 0 over RCCL, "
+                             "serial carry resolver there, carry-ins back, phase C on every rank, "
+                             "row blocks gathered); strong scaling, capped by the resolver",
+                     "stats": {k: (round(v, 4) if isinstance(v, float) else v)
+                               for k, v in (st or {}).items()}}
     if rank == 0:
         images = 1 if sharded else world
         value = images * W * H * args.steps / tmax
         work = WORK.get(f"{args.scene}:{args.size}:{args.depth}")
-        parity = mode == "parity" and args.depth > 0
+        rows_here = H if not sharded else (H + world - 1) // world
         if parity:
             dom_name, dom_ms = "k_resolve", phases["resolve_ms"]
             if piped and pipe_tim.get("resolve_ms"):   # the launches of the timed region
@@ -274,11 +348,15 @@ def main():
             render_ms = phases["phase_a_ms"] + phases["phase_c_ms"]
         else:
             dom_name, dom_ms = "k_render", phases["render_ms"]
-            dom_flop = work["render_flop_per_px"] * W * nrows if work else None
+            dom_flop = work["render_flop_per_px"] * W * rows_here if work else None
             render_ms = phases["render_ms"]
         ach = dom_flop / (dom_ms * 1e-3) / 1e12 if dom_flop and dom_ms else None
+        step_ms = tmax * 1e3 / args.steps
+        # per step: the dominant kernel's algorithmic work of one image over the step time
+        # (with frames in flight two resolvers overlap, so per-launch and per-step differ)
+        ach_step = (dom_flop * images / world) / (step_ms * 1e-3) / 1e12 if dom_flop else None
         traffic, traffic_src = pmc_traffic(dom_name, args.scene, args.size, args.depth, mode)
-        rach = (work["render_flop_per_px"] * W * nrows / (render_ms * 1e-3) / 1e12
+        rach = (work["render_flop_per_px"] * W * rows_here / (render_ms * 1e-3) / 1e12
                 if work and render_ms else None)
         line = {
             "metric": "primary rays/sec (= pixels/sec) at 4096x4096, quadric.scene",
@@ -287,17 +365,18 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(tmax * 1e3 / args.steps, 4),
+            "ms_per_step": round(step_ms, 4),
             "higher_is_better": True,
             "scaling": "strong" if sharded else "weak",
             "vs_baseline": None,
             "dtype": "f32+f64",
-            "data": "synthetic: the reference's own examples/quadric.scene (no dataset)",
+            "data": "synthetic: the reference's own examples/" + args.scene + ".scene (no dataset)",
             "config": {"workload": f"{args.scene}.scene {W}x{H}, bounce depth {args.depth} "
                                    f"(MAX_RECURSION {args.depth + 1}), {mode} mode"
                                    + (", byte-identical to C/raycast.c" if mode == "parity" else ""),
                        "mode": mode, "width": W, "height": H, "depth": args.depth,
-                       "parallelism": (f"rows-cyclic x{world} + RCCL all_gather" if sharded else
+                       "parallelism": (f"row-cyclic shards x{world}, RCCL gather in the library "
+                                       "(rc_render_sharded)" if sharded else
                                        (f"replicas x{world}" if world > 1 else "single GPU")),
                        "frames_in_flight": 2 if piped else 1},
             "phases_ms": {k: round(v, 4) for k, v in phases.items() if k.endswith("_ms")},
@@ -307,11 +386,14 @@ def main():
                          "achieved": round(ach, 4) if ach else None,
                          "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(ach / PEAK_FP64_TFLOPS, 5) if ach else None,
+                         "achieved_per_step": round(ach_step, 4) if ach_step else None,
+                         "frac_per_step": round(ach_step / PEAK_FP64_TFLOPS, 5) if ach_step else None,
                          "traffic": traffic,
                          "traffic_unit": "bytes per launch (HBM, PMC)",
                          "traffic_source": traffic_src,
-                         "note": ("serial carry chain: latency-bound, see DESIGN.md" if parity
-                                  else "throughput kernel")},
+                         "note": ("serial carry chain: latency-bound, see DESIGN.md; frac = per "
+                                  "launch, frac_per_step = one image's work over ms_per_step"
+                                  if parity else "throughput kernel")},
             "roofline_render": {"bound": "valu",
                                 "kernel": "k_phase_a+k_phase_c" if parity else "k_render",
                                 "kernel_ms": round(render_ms, 4),
@@ -319,17 +401,26 @@ def main():
                                 "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
                                 "frac": round(rach / PEAK_FP64_TFLOPS, 4) if rach else None},
             "roofline_hbm": {"bound": "hbm", "kernel": "framebuffer store (3 B/pixel)",
-                             "achieved": round(3 * W * nrows / (phases["total_ms"] * 1e-3) / 1e9, 3)
-                             if phases["total_ms"] else None,
+                             "achieved": round(3 * W * rows_here / (phases["total_ms"] * 1e-3) / 1e9, 3)
+                             if phases.get("total_ms") else None,
                              "peak": PEAK_HBM_GBS, "unit": "GB/s"},
         }
         if single:
             line["single_frame"] = single
-        if world == 1 and not sharded and not args.timed_only:
+        if shard_leg:
+            line["sharded_single_image"] = shard_leg
+        if group_err:
+            line["group_error"] = group_err
+        if sharded:
+            line["shard_stats"] = {k: (round(v, 4) if isinstance(v, float) else v)
+                                   for k, v in shard_stats.items()}
+        if world == 1 and not args.timed_only:
             line["end_to_end"] = end_to_end(pkg, scene, W, H, args.depth, mode)
         if world == 1 and not args.no_cpu_baseline and not args.timed_only:
             line["cpu_baseline"] = cpu_baseline(scene_path, args.size, args.depth)
         print(json.dumps(line), flush=True)
+    if group is not None:
+        group.close()
     if world > 1:
         dist.destroy_process_group()
 

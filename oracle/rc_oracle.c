@@ -416,6 +416,55 @@ int rco_render_cls(const json_data_t *js, int width, int height, int max_recursi
   return 0;
 }
 
+/* Selected pixels, each from a given carry-in (the row-shard protocol model, tests/
+ * test_dist.py): the pixel's colour, carry-out (next_intersecion after it), class (as in
+ * rco_render_cls) and zero-normalize events.  carry_in NULL = (0,0,0) for every pixel. */
+int rco_pixels(const json_data_t *js, int width, int height, int max_recursion, int mode,
+               int64_t n, const int64_t *pix, const float *carry_in, uint8_t *rgb,
+               float *carry_out, uint8_t *cls, int64_t *zero_events) {
+  rco_stats st;
+  octx c;
+  memset(&c, 0, sizeof c);
+  memset(&st, 0, sizeof st);
+  c.st = &st;
+  c.n = js->num_shapes;
+  c.m = js->num_lights;
+  shape_t *sh = (shape_t *)calloc((size_t)(c.n > 0 ? c.n : 1), sizeof(shape_t));
+  light_t *li = (light_t *)calloc((size_t)(c.m > 0 ? c.m : 1), sizeof(light_t));
+  if (!sh || !li) { free(sh); free(li); return -1; }
+  const shape_t *s = js->shapes_list;
+  for (int k = 0; k < c.n; k++) { if (!s) { free(sh); free(li); return -2; } sh[k] = *s; s = s->next; }
+  const light_t *l = js->lights_list;
+  for (int k = 0; k < c.m; k++) { if (!l) { free(sh); free(li); return -2; } li[k] = *l; l = l->next; }
+  c.shapes = sh;
+  c.lights = li;
+  o_build_phantom(&c);
+  const float ph = js->camera_height / (float)height;   /* C/raycast.c:109-110 */
+  const float pw = js->camera_width / (float)width;
+  for (int64_t i = 0; i < n; i++) {
+    const int x = (int)(pix[i] % width), y = (int)(pix[i] / width);
+    float d[3];
+    d[0] = (float)((0.0 - (double)js->camera_width / 2.0) + (double)pw * ((double)x + 0.5));
+    d[1] = (float)((0.0 + (double)js->camera_height / 2.0) - (double)ph * ((double)y + 0.5));
+    d[2] = -1.0f;
+    const int64_t z0 = st.zero_normalize;
+    o_normalize(&c, d, d);
+    for (int k = 0; k < 3; k++) c.carry[k] = carry_in ? carry_in[3 * i + k] : 0.0f;
+    float col[3];
+    pxinfo pi;
+    o_shoot(&c, d, max_recursion, mode, col, &pi, NULL);
+    for (int k = 0; k < 3; k++) {
+      rgb[3 * i + k] = o_quant(col[k]);
+      carry_out[3 * i + k] = c.carry[k];
+    }
+    cls[i] = (uint8_t)(pi.dep ? (pi.wrote ? 3 : 2) : (pi.wrote ? 1 : 0));
+    if (zero_events) zero_events[i] = st.zero_normalize - z0;
+  }
+  free(sh);
+  free(li);
+  return 0;
+}
+
 /* ------------------------------------------------ minimal scene reader (tests) -- */
 /* Reads the reference scene grammar (C/parse.c): one object per line, comma separated
  * `key: value` fields, vectors as [x, y, z].  Well-formed files only; no validation. */

@@ -412,16 +412,9 @@ def row_shard(height, rank, world):
     return rank, world, (height - rank + world - 1) // world
 
 
-def gather_rows(send, gathered, dist):
-    """All-gather each rank's padded row block ([rows_max, W, 3]) into
-    gathered ([world, rows_max, W, 3]).  With the "nccl" backend this is RCCL over xGMI."""
-    world, rows_max = gathered.shape[0], gathered.shape[1]
-    dist.all_gather_into_tensor(gathered.view(world * rows_max, *gathered.shape[2:]), send)
-    return gathered
-
-
 def deinterleave(gathered, height):
-    """Undo the row-cyclic partition: image row y = gathered[y % world][y // world]."""
+    """Undo the row-cyclic partition: image row y = gathered[y % world][y // world] (the
+    host-side statement of k_deinterleave, for the CPU protocol tests)."""
     world, rows_max, w, c = gathered.shape
     full = gathered.permute(1, 0, 2, 3).reshape(rows_max * world, w, c)
     return full[:height]

@@ -1,7 +1,18 @@
-"""CPU multi-process test (gloo, world_size 2) of the multi-GPU row-shard path used by
-bench.py in fast mode: row-cyclic partition -> per-rank row blocks -> all_gather ->
-de-interleave.  Each rank "renders" its rows with the CPU oracle (test infrastructure), so the
-collective logic is checked against a full-image render without a GPU."""
+"""CPU multi-process tests (gloo) of the row-shard protocol that rc_render_sharded runs over RCCL
+(raytracing-programs_amd/csrc/rc_shard.hip), with the CPU oracle standing in
+for the kernels (test infrastructure).
+
+* fast mode: row-cyclic partition (row y -> rank y % G), every rank's padded row block
+  gathered to rank 0 (a gather, as ncclGather does), de-interleaved there;
+* parity mode: the carry chain's exchange, record for record as the device runs it —
+  phase A on every rank (class, writer carry-outs, colours of the non-DEP pixels), the wire
+  records (per DEP entry: image pixel, the last writer before it in its row and that writer's
+  carry-out; per row: DEP count, segment starts inside the row, last writer / last DEP /
+  first DEP's writer and the last writer's carry-out) gathered to rank 0, which rebuilds the
+  image's scan order and segment table from them alone (k_shard_rows / k_row_scan /
+  k_shard_unpack), resolves the chain and scatters every rank its carry-ins; phase C on the
+  ranks; row blocks gathered.  The image must equal the oracle's whole-image render."""
+import ctypes
 import os
 import socket
 
@@ -11,7 +22,9 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from helpers import oracle_render, rc, scene_path
+from helpers import golden_key, golden_table, oracle_lib, oracle_render, p3_md5, rc, scene_path
+
+IDENT, WRITER = 0, 1   # oracle classes; 2 / 3 = DEP (first reflection missed)
 
 
 def _free_port():
@@ -22,31 +35,179 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, W, H, result_path):
+def pixels(scene, W, H, depth, mode, pix, cin=None):
+    """Oracle per-pixel shade (rco_pixels): rgb, carry-out, class, zero-normalize events."""
+    lib = oracle_lib()
+    lib.rco_pixels.argtypes = [ctypes.POINTER(rc.JsonDataT)] + [ctypes.c_int] * 4 + [
+        ctypes.c_int64] + [ctypes.c_void_p] * 6
+    pix = np.ascontiguousarray(pix, dtype=np.int64)
+    n = len(pix)
+    rgb = np.zeros((n, 3), np.uint8)
+    cout = np.zeros((n, 3), np.float32)
+    cls = np.zeros(n, np.uint8)
+    z = np.zeros(n, np.int64)
+    cin_p = None
+    if cin is not None:
+        cin = np.ascontiguousarray(cin, dtype=np.float32)
+        cin_p = cin.ctypes.data
+    assert lib.rco_pixels(ctypes.byref(scene.js), W, H, depth + 1, rc.MODES[mode], n,
+                          pix.ctypes.data, cin_p, rgb.ctypes.data, cout.ctypes.data,
+                          cls.ctypes.data, z.ctypes.data) == 0
+    return rgb, cout, cls, z
+
+
+def rank_phase_a(scene, W, H, depth, rank, G):
+    """A rank's phase A and wire records (k_phase_a + k_shard_pack)."""
+    rows = list(range(rank, H, G))
+    local = np.zeros((len(rows), W, 3), np.uint8)
+    entries, summaries = [], []
+    dep_pix = []
+    zero = 0
+    for j, y in enumerate(rows):
+        pix = np.arange(W, dtype=np.int64) + y * W
+        rgb, cout, cls, z = pixels(scene, W, H, depth, "parity", pix)
+        dep = cls >= 2
+        local[j][~dep] = rgb[~dep]
+        zero += int(z[~dep].sum())
+        lw = ld = wf = -1
+        nst = 0
+        first = True
+        for x in range(W):
+            if dep[x]:
+                if first:
+                    wf, first = lw, False
+                elif lw > ld:
+                    nst += 1   # a writer between the previous DEP and this one
+                kc = cout[lw] if lw >= 0 else np.zeros(3, np.float32)
+                entries.append((y * W + x, y * W + lw if lw >= 0 else -1, kc))
+                dep_pix.append((j, x))
+                ld = x
+            elif cls[x] == WRITER:
+                lw = x
+        summaries.append({"ndep": int(dep.sum()), "nstart": nst,
+                          "lastw": y * W + lw if lw >= 0 else -1,
+                          "lastd": y * W + ld if ld >= 0 else -1,
+                          "wfirst": y * W + wf if wf >= 0 else -1,
+                          "cw": cout[lw] if lw >= 0 else np.zeros(3, np.float32)})
+    return local, entries, summaries, dep_pix, zero
+
+
+def root_resolve(scene, W, H, depth, G, entries_all, rows_all):
+    """Rank 0: the image's scan order from the wire records alone, the segment table and the
+    exact chain (every DEP pixel's carry-in, in each rank's entry order)."""
+    row_off, pw, pd = {}, -1, -1
+    starts = []          # (global entry index, initial carry)
+    order = []           # (rank, local index) in image scan order
+    for y in range(H):
+        g, j = y % G, y // G
+        r = rows_all[g][j]
+        loff = sum(rows_all[g][q]["ndep"] for q in range(j))
+        prev = pd
+        for i in range(r["ndep"]):
+            pix, kin, kc = entries_all[g][loff + i]
+            kw = kin if kin >= 0 else pw
+            if prev < 0 or kw > prev:
+                if kin >= 0:
+                    c0 = kc
+                elif pw >= 0:
+                    yw = pw // W
+                    c0 = rows_all[yw % G][yw // G]["cw"]
+                else:
+                    c0 = np.zeros(3, np.float32)
+                starts.append((len(order), np.asarray(c0, np.float32)))
+            order.append((g, loff + i))
+            prev = pix
+        if r["lastw"] >= 0:
+            pw = r["lastw"]
+        if r["lastd"] >= 0:
+            pd = r["lastd"]
+    cin = [np.zeros((len(e), 3), np.float32) for e in entries_all]
+    bounds = [s for s, _ in starts] + [len(order)]
+    for k, (s0, c0) in enumerate(starts):
+        c = c0
+        for idx in range(s0, bounds[k + 1]):   # the chain: one entry at a time
+            g, li = order[idx]
+            cin[g][li] = c
+            _, cout, _, _ = pixels(scene, W, H, depth, "parity",
+                                   [entries_all[g][li][0]], c[None, :])
+            c = cout[0]
+    return cin
+
+
+def _worker(rank, world, port, name, W, H, depth, mode, result_path):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    scene = rc.Scene.from_file(scene_path("quadric"))
-    full, _ = oracle_render(scene, W, H, 6, "fast")
+    scene = rc.Scene.from_file(scene_path(name))
     row0, step, nrows = rc.row_shard(H, rank, world)
     rows_max = (H + world - 1) // world
     send = torch.zeros((rows_max, W, 3), dtype=torch.uint8)
-    send[:nrows] = torch.from_numpy(full[row0::step])   # this rank's rows, as the GPU renders them
-    gathered = torch.empty((world, rows_max, W, 3), dtype=torch.uint8)
-    rc.gather_rows(send, gathered, dist)
+    if mode == "fast":
+        pix = np.concatenate([np.arange(W) + y * W for y in range(row0, H, step)] or [[]])
+        rgb, _, _, z = pixels(scene, W, H, depth, "fast", pix.astype(np.int64))
+        send[:nrows] = torch.from_numpy(rgb.reshape(nrows, W, 3))
+        zero = int(z.sum())
+    else:
+        local, entries, summaries, dep_pix, zero = rank_phase_a(scene, W, H, depth, rank, world)
+        gathered = [None] * world if rank == 0 else None
+        dist.gather_object((entries, summaries), gathered, dst=0)
+        cin_lists = None
+        if rank == 0:
+            cin_lists = root_resolve(scene, W, H, depth, world, [g[0] for g in gathered],
+                                     [g[1] for g in gathered])
+        mine = [None]
+        dist.scatter_object_list(mine, cin_lists, src=0)
+        cin = mine[0]
+        if len(entries):   # phase C on the rank
+            rgb, _, _, z = pixels(scene, W, H, depth, "parity", [e[0] for e in entries], cin)
+            for k, (j, x) in enumerate(dep_pix):
+                local[j, x] = rgb[k]
+            zero += int(z.sum())
+        send[:nrows] = torch.from_numpy(local)
+    blocks = [torch.empty_like(send) for _ in range(world)] if rank == 0 else None
+    dist.gather(send, blocks, dst=0)
+    zs = [None] * world if rank == 0 else None
+    dist.gather_object(zero, zs, dst=0)
     if rank == 0:
-        img = rc.deinterleave(gathered, H).numpy()
+        img = rc.deinterleave(torch.stack(blocks), H).numpy()
         np.save(result_path, img)
-        np.save(result_path + ".ref.npy", full)
+        np.save(result_path + ".zero.npy", np.array(sum(zs)))
     dist.destroy_process_group()
+
+
+def run_world(tmp_path, world, name, W, H, depth, mode):
+    out = str(tmp_path / f"img_{world}_{mode}.npy")
+    mp.spawn(_worker, args=(world, _free_port(), name, W, H, depth, mode, out), nprocs=world,
+             join=True)
+    return np.load(out), int(np.load(out + ".zero.npy"))
 
 
 @pytest.mark.parametrize("W,H", [(40, 31), (17, 2)])
 def test_row_cyclic_gather_world2(tmp_path, W, H):
-    world = 2
-    out = str(tmp_path / "img.npy")
-    mp.spawn(_worker, args=(world, _free_port(), W, H, out), nprocs=world, join=True)
-    np.testing.assert_array_equal(np.load(out), np.load(out + ".ref.npy"))
+    scene = rc.Scene.from_file(scene_path("quadric"))
+    img, zero = run_world(tmp_path, 2, "quadric", W, H, 6, "fast")
+    want, st = oracle_render(scene, W, H, 6, "fast")
+    np.testing.assert_array_equal(img, want)
+    assert zero == st["zero_normalize"]
+
+
+@pytest.mark.parametrize("world,name,W,H,depth", [(2, "quadric", 48, 40, 6),
+                                                 (3, "reflection", 64, 64, 4),
+                                                 (2, "simple", 64, 64, 6),
+                                                 (3, "quadric", 23, 2, 6)])
+def test_parity_shard_protocol(tmp_path, world, name, W, H, depth):
+    """The parity exchange, modelled on CPU: byte-identical to the whole-image oracle (and to
+    the reference's md5 where a golden exists)."""
+    scene = rc.Scene.from_file(scene_path(name))
+    img, zero = run_world(tmp_path, world, name, W, H, depth, "parity")
+    want, st = oracle_render(scene, W, H, depth, "parity")
+    assert st["dep_pixels"] > 0, "the case must exercise the carry chain"
+    np.testing.assert_array_equal(img, want)
+    assert zero == st["zero_normalize"]
+    key = golden_key(name, W, H, depth, "parity")
+    table = golden_table()
+    if key in table:
+        assert p3_md5(img) == table[key]["md5"]
 
 
 def test_row_shard_partition():
