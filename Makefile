@@ -29,7 +29,7 @@ HIP_SRCS  := $(SRC)/rc_kernels.hip $(SRC)/rc_api.hip $(SRC)/rc_shard.hip
 HIP_HDRS  := $(SRC)/rc_device.hpp $(SRC)/rc_kernels.h $(SRC)/rc_runtime.h $(SRC)/rc_scene.h include/raycast_hip.h
 FRONT_SRC := $(SRC)/front/parse.c $(SRC)/front/objects.c $(SRC)/front/ppm.c
 
-.PHONY: all oracle ref clean stamps
+.PHONY: all oracle ref clean stamps sanitize
 all: $(LIB)/libraycast_hip.so $(LIB)/libraycast_front.so $(BIN)/raytrace oracle
 
 $(OBJ)/%.o: $(SRC)/%.hip $(HIP_HDRS)
@@ -84,3 +84,16 @@ $(OBJ)/t16_kernels.o: $(SRC)/rc_kernels.hip $(HIP_HDRS)
 	$(HIPCC) $(HIPFLAGS) -DRC_TILE_W=16 -DRC_TILE_STAGE=1 -c $< -o $@
 $(LIB)/libraycast_hip_%.so: $(OBJ)/%_kernels.o $(OBJ)/rc_api.o $(OBJ)/rc_shard.o $(OBJ)/rc_scene.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -o $@ $(HIPLIBS)
+
+# ASan + UBSan builds of the host C (tests/test_sanitize.py; SURVEY.md §5: the CPU restatement
+# must not rely on UB): the oracle's CLI and the front end (parse / lists / P3 writer) driven
+# by tests/tools/front_check.c.  Host code only; no GPU code is sanitized.
+SAN     := -fsanitize=address,undefined -fno-sanitize-recover=undefined -fno-omit-frame-pointer -g
+SAN_OUT := build/sanitize
+sanitize: $(SAN_OUT)/oracle_raytrace $(SAN_OUT)/front_check
+$(SAN_OUT)/oracle_raytrace: oracle/oracle_main.c oracle/rc_oracle.c oracle/rc_oracle.h include/raycast_hip.h
+	@mkdir -p $(SAN_OUT)
+	$(CC) -O1 -ffp-contract=off $(SAN) -Iinclude oracle/oracle_main.c oracle/rc_oracle.c -o $@ -lm
+$(SAN_OUT)/front_check: tests/tools/front_check.c $(FRONT_SRC) include/raycast_hip.h
+	@mkdir -p $(SAN_OUT)
+	$(CC) -O1 -ffp-contract=off $(SAN) -Iinclude -I$(SRC) tests/tools/front_check.c $(FRONT_SRC) -o $@ -lm -lpthread

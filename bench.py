@@ -359,7 +359,9 @@ def main():
         rach = (work["render_flop_per_px"] * W * rows_here / (render_ms * 1e-3) / 1e12
                 if work and render_ms else None)
         line = {
-            "metric": "primary rays/sec (= pixels/sec) at 4096x4096, quadric.scene",
+            "metric": ("primary rays/sec (= pixels/sec) at 4096x4096, quadric.scene"
+                       if (args.scene, W) == ("quadric", 4096) else
+                       f"primary rays/sec (= pixels/sec) at {W}x{H}, {args.scene}.scene"),
             "value": round(value, 1),
             "unit": "rays/s",
             "n_gpus": world,

@@ -180,6 +180,24 @@ def test_cli_dropin(tmp_path, table):
     assert file_md5(str(out)) == table["quadric:256x256:d4:fast"]["md5"]
 
 
+OPTB = os.path.join(ROOT, "oracle", "_ref", "raytrace_optb")
+
+
+@pytest.mark.skipif(not os.path.exists(OPTB), reason="oracle/_ref not built (make ref)")
+def test_option_b_reference_main(tmp_path, table):
+    """INTEGRATION.md Option B: the reference's own program (C/raycast.c:19-69 main, its own
+    parse.c / ppm.c) with its raycast() fenced off by #ifndef RAYCAST_HIP (oracle/Makefile),
+    linked against libraycast_hip.so: C1 and C4 files md5-equal to the reference's."""
+    for scene, n, key in [("simple", 256, "simple:256x256:d6:parity"),
+                          ("quadric", 4096, "quadric:4096x4096:d6:parity")]:
+        out = tmp_path / f"{scene}.ppm"
+        r = subprocess.run([OPTB, str(n), str(n), scene_path(scene), str(out)],
+                           capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr
+        assert "image with" in r.stdout
+        assert file_md5(str(out)) == table[key]["md5"], key
+
+
 def test_device_render_matches_host(scenes, table):
     """rc_render_device (device-resident output, the bench path) writes the same bytes."""
     torch = pytest.importorskip("torch")
