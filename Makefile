@@ -54,14 +54,15 @@ $(BIN)/raytrace: $(SRC)/front/raytrace_main.c $(LIB)/libraycast_front.so $(LIB)/
 	@mkdir -p $(BIN)
 	$(CC) $(CFLAGS) $< -L$(LIB) -lraycast_front -lraycast_hip -Wl,-rpath,'$$ORIGIN/../lib' -o $@
 
-# diagnostic build with in-kernel cycle stamps (RC_HIP_LIB=libraycast_hip_stamps.so)
+# diagnostic build with in-kernel cycle stamps and the RC_RESOLVE_TRACE / RC_SIDE_STATS dumps
+# (RC_HIP_LIB=libraycast_hip_stamps.so); the product library reads only RAYCAST_* options
 stamps: $(LIB)/libraycast_hip_stamps.so
 $(OBJ)/stamps_kernels.o: $(SRC)/rc_kernels.hip $(HIP_HDRS)
 	@mkdir -p $(OBJ)
-	$(HIPCC) $(HIPFLAGS) -DRC_STAMPS=1 -c $< -o $@
+	$(HIPCC) $(HIPFLAGS) -DRC_STAMPS=1 -DRC_DIAG=1 -c $< -o $@
 $(OBJ)/stamps_api.o: $(SRC)/rc_api.hip $(HIP_HDRS)
 	@mkdir -p $(OBJ)
-	$(HIPCC) $(HIPFLAGS) -DRC_STAMPS=1 -c $< -o $@
+	$(HIPCC) $(HIPFLAGS) -DRC_STAMPS=1 -DRC_DIAG=1 -c $< -o $@
 $(LIB)/libraycast_hip_stamps.so: $(OBJ)/stamps_kernels.o $(OBJ)/stamps_api.o $(OBJ)/rc_shard.o $(OBJ)/rc_scene.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -o $@ $(HIPLIBS)
 

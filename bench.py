@@ -187,6 +187,9 @@ def main():
     ap.add_argument("--inflight", type=int, default=2, choices=[1, 2],
                     help="parity frames in flight: 2 = rc_frame_submit (the next frame's pixel "
                          "phases beside this frame's resolver), 1 = one rc_render_device per step")
+    ap.add_argument("--tune", action="append", default=[], metavar="FIELD=VALUE",
+                    help="schedule experiment: rc_set_tuning field (repeatable; see "
+                         "include/raycast_hip.h rc_tuning); the default is the product schedule")
     ap.add_argument("--shard", action="store_true",
                     help="N>1 parity: time the row-sharded single image (rc_render_sharded) as "
                          "the step instead of N replicas")
@@ -208,6 +211,8 @@ def main():
         else:
             dist.init_process_group(backend)
     pkg = load_pkg()
+    if args.tune:
+        pkg.set_tuning(**{k: int(v) for k, v in (t.split("=", 1) for t in args.tune)})
     scene_path = os.path.join(ROOT, "tests", "golden", "scenes", args.scene + ".scene")
     scene = pkg.Scene.from_file(scene_path)
     W = H = args.size
@@ -382,6 +387,8 @@ def main():
                                        (f"replicas x{world}" if world > 1 else "single GPU")),
                        "frames_in_flight": 2 if piped else 1},
             "phases_ms": {k: round(v, 4) for k, v in phases.items() if k.endswith("_ms")},
+            "tuning": ({t.split("=", 1)[0]: int(t.split("=", 1)[1]) for t in args.tune}
+                       if args.tune else "default"),
             "dep_pixels": tim.get("dep_pixels"),
             "roofline": {"bound": "valu", "kernel": dom_name,
                          "kernel_ms": round(dom_ms, 4),

@@ -213,6 +213,44 @@ typedef struct rc_phase_stats {
 int rc_profile_begin(void);
 int rc_profile_end(rc_phase_stats *out);
 
+/* ---- schedule tuning (process-wide) -------------------------------------------------
+ * The product's schedule is fixed by rc_default_tuning(); these fields exist so tests and
+ * experiments can select the measured alternatives explicitly instead of
+ * through the environment.  rc_set_tuning validates every field (returns -1 and changes
+ * nothing when one is out of range); the resolver's co-residency limits are enforced on
+ * top of it.  Takes effect at the next render (the frame pipeline's layout at its next
+ * build: rc_pipe_reset). */
+typedef struct rc_tuning {
+  int side;               /* 1: a lone parity frame's phase C runs beside the resolver     */
+  int split_shade;        /* 1: phase A's colours move beside the resolver (needs side)    */
+  int resolve_shared;     /* 1: no one-resolver-workgroup-per-CU LDS reservation           */
+  int resolve_lds_kb;     /* resolver LDS reservation in KiB, 0 = by path (96 / 56)        */
+  int resolve_grid;       /* resolver workgroups, 0 = resident capacity (>= 8 otherwise)   */
+  int team_blocks;        /* long-segment team workgroups, -1 = by path (128 / 3/8 grid)   */
+  int helpers;            /* dense-run helper workgroups (0..64)                            */
+  int hand_run;           /* changes in a row before a wave hands its run to a helper       */
+  int long_len;           /* segments of >= long_len entries go to the team                 */
+  int wave_k;             /* clean cooperative steps before a wave window returns to LANE   */
+  int resolve_k;          /* the same for the team leader's block window                     */
+  int coop;               /* 1: cooperative (lanes per entry) evaluator                      */
+  int dep_fast;           /* 1: clean DEP entries take phase A's primary shade               */
+  int o0;                 /* 1: primary rays through the origin-zero intersection forms      */
+  int phase_c_finish;     /* 1: phase C after the resolver through k_finish's batch claims   */
+  int single_res_cus;     /* lone frames: resolver sized for this many CUs, 0 = all          */
+  int pipe_res_cus;       /* frames in flight: resolver partition CUs, 0 = by image size     */
+  int pipe_resolvers;     /* frames in flight: resolver lanes (1..4)                          */
+  int pipe_slots;         /* frames in flight: frame workspaces (lanes+1 .. 8)                */
+  int pipe_timing;        /* 1: resolver timing events per pipelined frame                   */
+  int pipe_slotstreams;   /* 1: one stream per slot (A, compaction, C in turn)               */
+  int overlap_d2h;        /* 1: rc_render's copy overlaps the resolver (parity)              */
+  int staged_d2h;         /* 1: pinned bounce buffers + host pool; 0: runtime pageable copy  */
+  int prefault;           /* 1: fault the caller's pixmap in while the GPU renders           */
+  int copy_threads;       /* host copy pool threads (1..32; fixed at the pool's first use)   */
+} rc_tuning;
+void rc_default_tuning(rc_tuning *t);
+int rc_set_tuning(const rc_tuning *t);
+void rc_get_tuning(rc_tuning *t);
+
 /* ---- multi-GPU row shards ----------------------------------------------
  * Rows are dealt cyclically (image row y -> rank y % G).  Every rank renders its rows; the
  * root (rank 0) gathers the row blocks over RCCL (ncclGather over xGMI) and undoes the

@@ -81,6 +81,17 @@ class RcShardStats(ctypes.Structure):
                 ("image_bytes", ctypes.c_int64)]
 
 
+TUNING_FIELDS = ["side", "split_shade", "resolve_shared", "resolve_lds_kb", "resolve_grid",
+                 "team_blocks", "helpers", "hand_run", "long_len", "wave_k", "resolve_k", "coop",
+                 "dep_fast", "o0", "phase_c_finish", "single_res_cus", "pipe_res_cus",
+                 "pipe_resolvers", "pipe_slots", "pipe_timing", "pipe_slotstreams", "overlap_d2h",
+                 "staged_d2h", "prefault", "copy_threads"]
+
+
+class RcTuning(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int) for n in TUNING_FIELDS]
+
+
 assert ctypes.sizeof(ShapeT) == 104 and ctypes.sizeof(LightT) == 72
 
 # the functions include/raycast_hip.h declares, per library
@@ -89,7 +100,8 @@ HIP_EXPORTS = ["raycast", "rc_default_options", "rc_scene_create", "rc_scene_des
                "rc_profile_begin", "rc_profile_end", "rc_version", "rc_frame_submit",
                "rc_frames_wait", "rc_pipe_reset", "rc_group_unique_id", "rc_group_create_rank",
                "rc_group_create_local", "rc_group_destroy", "rc_group_size",
-               "rc_group_transport", "rc_render_sharded", "rc_group_last_stats"]
+               "rc_group_transport", "rc_render_sharded", "rc_group_last_stats",
+               "rc_default_tuning", "rc_set_tuning", "rc_get_tuning"]
 FRONT_EXPORTS = ["add_new_sphere", "add_new_plane", "add_new_quadric", "free_shape_list",
                  "free_light_list", "add_new_spot_light", "add_new_point_light", "parse_json",
                  "set_to_black", "ppm_WriteOutP3", "ppm_clamp"]
@@ -149,6 +161,11 @@ def hip_lib():
                                       ctypes.POINTER(RcOptions), ctypes.c_void_p,
                                       ctypes.POINTER(RcTiming)]
     lib.rc_group_last_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(RcShardStats)]
+    lib.rc_default_tuning.argtypes = [ctypes.POINTER(RcTuning)]
+    lib.rc_default_tuning.restype = None
+    lib.rc_get_tuning.argtypes = [ctypes.POINTER(RcTuning)]
+    lib.rc_get_tuning.restype = None
+    lib.rc_set_tuning.argtypes = [ctypes.POINTER(RcTuning)]
     return lib
 
 
@@ -231,6 +248,41 @@ class Scene:
             self.close()
         except Exception:
             pass
+
+
+def get_tuning(default=False):
+    """The process-wide schedule tuning (rc_get_tuning / rc_default_tuning) as a dict."""
+    t = RcTuning()
+    (hip_lib().rc_default_tuning if default else hip_lib().rc_get_tuning)(ctypes.byref(t))
+    return {n: getattr(t, n) for n in TUNING_FIELDS}
+
+
+def set_tuning(**fields):
+    """Change tuning fields (the rest keep their current values); rc_set_tuning validates."""
+    cur = get_tuning()
+    unknown = set(fields) - set(cur)
+    if unknown:
+        raise KeyError(f"unknown tuning fields {sorted(unknown)}")
+    cur.update(fields)
+    t = RcTuning(**cur)
+    if hip_lib().rc_set_tuning(ctypes.byref(t)) != 0:
+        raise ValueError(f"rc_set_tuning rejected {fields}")
+
+
+class tuned:
+    """Context manager: `with tuned(side=0): ...` renders with the given tuning, then restores."""
+
+    def __init__(self, **fields):
+        self.fields = fields
+
+    def __enter__(self):
+        self.saved = get_tuning()
+        set_tuning(**self.fields)
+        return self
+
+    def __exit__(self, *exc):
+        set_tuning(**self.saved)
+        return False
 
 
 def options(depth=6, mode="parity", gpus=1, device=0):

@@ -32,6 +32,38 @@ namespace rcrt {
 
 DevCtx g_ctx[kMaxDevices];
 std::mutex g_ctx_mu;
+
+rc_tuning default_tuning() {
+  rc_tuning t;
+  t.side = 1;
+  t.split_shade = 0;
+  t.resolve_shared = 0;
+  t.resolve_lds_kb = 0;
+  t.resolve_grid = 0;
+  t.team_blocks = -1;
+  t.helpers = 8;
+  t.hand_run = 512;
+  t.long_len = 32768;
+  t.wave_k = 2;
+  t.resolve_k = 1;
+  t.coop = 1;
+  t.dep_fast = 1;
+  t.o0 = 1;
+  t.phase_c_finish = 0;
+  t.single_res_cus = 0;
+  t.pipe_res_cus = 0;
+  t.pipe_resolvers = 2;
+  t.pipe_slots = 4;
+  t.pipe_timing = 1;
+  t.pipe_slotstreams = 0;
+  t.overlap_d2h = 1;
+  t.staged_d2h = 1;
+  t.prefault = 1;
+  t.copy_threads = 8;
+  return t;
+}
+rc_tuning g_tune = default_tuning();
+const rc_tuning& tune() { return g_tune; }
 double g_last_kernel_ms = 0.0;
 
 int ctx_get(int device, DevCtx** out) {
@@ -94,8 +126,7 @@ class HostPool {
 
  private:
   HostPool() {
-    int t = 7;
-    if (const char* e = std::getenv("RC_COPY_THREADS")) t = std::atoi(e) - 1;
+    int t = tune().copy_threads - 1;
     if (t < 0) t = 0;
     if (t > 31) t = 31;
     nthreads_ = t;
@@ -127,7 +158,7 @@ class HostPool {
 };
 
 int copy_to_host(DevCtx& c, uint8_t* host, const uint8_t* dev, size_t bytes, hipStream_t st) {
-  if (std::getenv("RC_PLAIN_D2H")) {   // the runtime's pageable copy
+  if (!tune().staged_d2h) {   // the runtime's pageable copy
     HIP_TRY(hipMemcpyAsync(host, dev, bytes, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     return 0;
@@ -161,7 +192,7 @@ int copy_to_host(DevCtx& c, uint8_t* host, const uint8_t* dev, size_t bytes, hip
 // Fault the caller's fresh pixmap in (C/raycast.c:52-53 mallocs it) over the host pool while the
 // GPU renders, instead of inside the copy (every byte is overwritten afterwards).
 void prefault(uint8_t* p, size_t n) {
-  if (!n || std::getenv("RC_NO_PREFAULT")) return;
+  if (!n || !tune().prefault) return;
   HostPool::get().run([&](int part, int parts) {
     const size_t per = ((n + parts - 1) / parts + 4095) & ~(size_t)4095;
     const size_t a = (size_t)part * per, b = a + per < n ? a + per : n;
@@ -233,6 +264,36 @@ extern "C" {
 
 const char* rc_version(void) { return RC_VERSION; }
 
+void rc_default_tuning(rc_tuning* t) {
+  if (t) *t = default_tuning();
+}
+
+void rc_get_tuning(rc_tuning* t) {
+  if (t) *t = g_tune;
+}
+
+int rc_set_tuning(const rc_tuning* t) {
+  if (!t) return -1;
+  auto in = [](int v, int lo, int hi) { return v >= lo && v <= hi; };
+  const bool ok =
+      in(t->side, 0, 1) && in(t->split_shade, 0, 1) && in(t->resolve_shared, 0, 1) &&
+      in(t->resolve_lds_kb, 0, 152) && (t->resolve_grid == 0 || in(t->resolve_grid, 8, 1 << 16)) &&
+      in(t->team_blocks, -1, 256) && in(t->helpers, 0, rc::kDenseSlots) &&
+      in(t->hand_run, 1, 1 << 30) && in(t->long_len, 64, 1 << 30) && in(t->wave_k, 1, 64) &&
+      in(t->resolve_k, 1, 64) && in(t->coop, 0, 1) && in(t->dep_fast, 0, 1) && in(t->o0, 0, 1) &&
+      in(t->phase_c_finish, 0, 1) && in(t->single_res_cus, 0, 1 << 16) &&
+      in(t->pipe_res_cus, 0, 1 << 16) && in(t->pipe_resolvers, 1, 4) && in(t->pipe_slots, 1, 8) &&
+      in(t->pipe_timing, 0, 1) && in(t->pipe_slotstreams, 0, 1) && in(t->overlap_d2h, 0, 1) &&
+      in(t->staged_d2h, 0, 1) && in(t->prefault, 0, 1) && in(t->copy_threads, 1, 32) &&
+      !(t->split_shade && !t->side);
+  if (!ok) {
+    std::fprintf(stderr, "Error: rc_set_tuning: a field is out of range\n");
+    return -1;
+  }
+  g_tune = *t;
+  return 0;
+}
+
 double rc_last_kernel_ms(void) { return g_last_kernel_ms; }
 
 void rc_default_options(rc_options* opt, int use_env) {
@@ -300,7 +361,7 @@ int upload_scene(FrameBufs& b, hipStream_t stream, const rc_scene* s, rc::Launch
   ls.cam_h = h->cam_h;
   ls.refl_mask = 0;
   ls.has_quadric = 0;
-  ls.o0_ok = h->o0_ok && !std::getenv("RC_NO_O0");
+  ls.o0_ok = h->o0_ok && tune().o0;
   const rc_shape* hs = (const rc_shape*)((const char*)h + h->off_shapes);
   for (int k = 0; k < h->n && k < 64; ++k)
     if (hs[k].refl > 0.0f) ls.refl_mask |= 1ull << k;
@@ -309,7 +370,7 @@ int upload_scene(FrameBufs& b, hipStream_t stream, const rc_scene* s, rc::Launch
   // Clean DEP entries' colour = phase A's primary shade exactly when every bounce level's
   // shade of them is zero: the phantom (shapes_list[-1], index n) is black, and the
   // reflectivity product T stays finite (0 * T == 0).
-  ls.dep_fast = !(hs[h->n].opacity > 0.0f) && !std::getenv("RC_NO_DEP_FAST");
+  ls.dep_fast = !(hs[h->n].opacity > 0.0f) && tune().dep_fast;
   for (int k = 0; k < h->n; ++k)
     if (!(std::fabs(hs[k].refl) < 1.0e5f)) ls.dep_fast = 0;
   return 0;
@@ -346,9 +407,10 @@ int ensure_parity(DevCtx& c, FrameBufs& b, int W, int H, rc::ParityWork& w, int 
   // the longest segments outnumber one-per-CU's waves and the chains that start late set the
   // resolver's time (measured: 4.9e9 -> 5.4e9 rays/s with frames in flight, 6.37 -> 6.49 ms
   // for a lone frame).
-  const int one_per_cu = std::getenv("RC_RESOLVE_SHARED") ? 0 : 1;
+  const rc_tuning& tu = tune();
+  const int one_per_cu = tu.resolve_shared ? 0 : 1;
   int lds = !one_per_cu ? 0 : piped ? 56 * 1024 : 96 * 1024;
-  if (const char* e = std::getenv("RC_RESOLVE_LDS_KB")) lds = std::atoi(e) * 1024;
+  if (tu.resolve_lds_kb > 0) lds = tu.resolve_lds_kb * 1024;
   int slot = 0;
   while (slot < DevCtx::kResCache && c.res_lds[slot] != lds && c.res_blocks[slot]) ++slot;
   if (slot == DevCtx::kResCache) slot = 0;
@@ -377,9 +439,9 @@ int ensure_parity(DevCtx& c, FrameBufs& b, int W, int H, rc::ParityWork& w, int 
   w.rstream = nullptr;
   w.pstream = nullptr;
   w.rready = w.rdone = w.rt0 = w.rt1 = nullptr;
-  w.split_shade = std::getenv("RC_SPLIT_SHADE") ? 1 : 0;
+  w.split_shade = tu.split_shade ? 1 : 0;
   if (piped) w.split_shade = 0;   // phase C after the resolver, on the pixel partition
-  if (!piped && !std::getenv("RC_NO_SIDE")) {   // phase C overlapped with the resolver
+  if (!piped && tu.side) {   // phase C overlapped with the resolver
     if (!c.side) {
       if (hipStreamCreateWithFlags(&c.side, hipStreamNonBlocking) != hipSuccess ||
           hipEventCreateWithFlags(&c.fork, hipEventDisableTiming) != hipSuccess ||
@@ -402,40 +464,40 @@ int ensure_parity(DevCtx& c, FrameBufs& b, int W, int H, rc::ParityWork& w, int 
   // The team spins on a counter barrier: its blocks (the first of the grid) and the grid as
   // a whole must be co-resident, so the grid never exceeds the resident capacity.
   w.resolve_blocks = c.resident_blocks / c.cus * res_cus;   // whole CUs' worth
-  if (const char* e = std::getenv("RC_RESOLVE_GRID")) {     // experiments: a smaller grid
-    const int g = std::atoi(e);
-    if (g >= 8 && g < w.resolve_blocks) w.resolve_blocks = g;
-  }
+  if (tu.resolve_grid >= 8 && tu.resolve_grid < w.resolve_blocks)   // experiments: a smaller grid
+    w.resolve_blocks = tu.resolve_grid;
   w.resolve_lds = c.resident_lds;
   // team size: 128 of a whole-device grid; 3/8 of a pipelined resolver's grid (64 -> 24:
   // measured 4.77e9 vs 4.50e9 rays/s at 32, 4.49e9 at 20)
   w.team_blocks = piped ? w.resolve_blocks * 3 / 8 : 128;
-  if (const char* e = std::getenv("RC_TEAM_BLOCKS")) w.team_blocks = std::atoi(e);
+  if (tu.team_blocks >= 0) w.team_blocks = tu.team_blocks;
   if (w.team_blocks > 256) w.team_blocks = 256;
   if (w.team_blocks > w.resolve_blocks / 2) w.team_blocks = w.resolve_blocks / 2;
   // helper blocks for handed-off dense runs (k_resolve): 8 of the grid
-  w.helpers = std::getenv("RC_HELPERS") ? std::atoi(std::getenv("RC_HELPERS")) : 8;
+  w.helpers = tu.helpers;
   if (w.helpers < 0) w.helpers = 0;
   if (w.helpers > rc::kDenseSlots) w.helpers = rc::kDenseSlots;   // one ring slot per helper
   if (w.team_blocks + w.helpers > w.resolve_blocks * 3 / 4) w.helpers = 0;
-  w.hand_run = std::getenv("RC_HAND_RUN") ? std::atoi(std::getenv("RC_HAND_RUN")) : 512;
-  w.long_len = std::getenv("RC_LONG_LEN") ? std::atoi(std::getenv("RC_LONG_LEN")) : 32768;
-  w.wave_k = std::getenv("RC_WAVE_K") ? std::atoi(std::getenv("RC_WAVE_K")) : 2;
-  w.resolve_k = std::getenv("RC_RESOLVE_K") ? std::atoi(std::getenv("RC_RESOLVE_K")) : 1;
+  w.hand_run = tu.hand_run;
+  w.long_len = tu.long_len;
+  w.wave_k = tu.wave_k;
+  w.resolve_k = tu.resolve_k;
   w.coop_group = 0;
-  if (!std::getenv("RC_NO_COOP") && b.scene_src) {
+  if (tu.coop && b.scene_src) {
     const int n = ((const rc_packed_header*)b.scene_src)->n;
     int g = 4;   // groups of >= 4 lanes: the evaluator is specialised for 4, 8 and 16
     while (g < n) g <<= 1;
     if (n >= 1 && g <= 64) w.coop_group = g;
   }
   w.trace = nullptr;
+#if RC_DIAG   // diagnostic build (make stamps): per-segment resolver trace
   if (std::getenv("RC_RESOLVE_TRACE")) {
     if (b.trace.ensure(P * 7 * sizeof(unsigned))) return -1;
     w.trace = (unsigned*)b.trace.p;
   }
+#endif
   w.phase_c_blocks = (piped ? c.cus - res_cus : c.cus) * 8;
-  w.phase_c_finish = std::getenv("RC_PHASE_C_FINISH") ? 1 : 0;
+  w.phase_c_finish = tu.phase_c_finish ? 1 : 0;
   return 0;
 }
 
@@ -467,8 +529,8 @@ int enqueue_render(DevCtx& c, const rc_scene* s, int W, int H, int row0, int row
     return -1;
   }
   rc::ParityWork w{};
-  int res_cus = c.cus;   // diagnostic: RC_SINGLE_RES_CUS sizes the resolver like a pipeline lane's
-  if (const char* e = std::getenv("RC_SINGLE_RES_CUS")) res_cus = std::atoi(e);
+  int res_cus = c.cus;   // experiment: single_res_cus sizes the resolver like a pipeline lane's
+  if (tune().single_res_cus > 0) res_cus = tune().single_res_cus;
   if (res_cus < 8 || res_cus > c.cus) res_cus = c.cus;
   if (ensure_parity(c, c.fb, W, H, w, res_cus)) {
     std::fprintf(stderr, "Error: out of device memory for the parity workspace\n");
@@ -560,6 +622,7 @@ void fill_device_timing(DevCtx& c, const rc_options* opt, rc_timing* t) {
     int cnt[4] = {0, 0, 0, 0};
     if (hipMemcpy(cnt, c.fb.counters.p, sizeof cnt, hipMemcpyDeviceToHost) == hipSuccess)
       t->dep_pixels = cnt[2];
+#if RC_DIAG
     if (std::getenv("RC_SIDE_STATS")) {
       int cc[16];
       if (hipMemcpy(cc, c.fb.counters.p, sizeof cc, hipMemcpyDeviceToHost) == hipSuccess)
@@ -626,6 +689,7 @@ void fill_device_timing(DevCtx& c, const rc_options* opt, rc_timing* t) {
       }
 #endif
     }
+#endif  // RC_DIAG
   }
 }
 
@@ -721,18 +785,17 @@ int pipe_init(DevCtx& c, long long pixels) {
   // phases are the bound (reflection 2048^2 d4 6.9e9 -> 7.9e9, simple 1024^2 d6 3.5e9 -> 3.7e9
   // rays/s vs half); half up to 32 Mpixel (quadric 4096^2: 5.7e9 at 128 CUs, 5.1e9 at 112);
   // 3/8 above (quadric 8192^2: 7.4e9 at 96 CUs, 6.4e9 at 128, 6.0e9 at 80).
+  const rc_tuning& tu = tune();
   int res = pixels < (8ll << 20) ? c.cus / 4 : pixels < (32ll << 20) ? c.cus / 2 : c.cus * 3 / 8;
-  if (const char* e = std::getenv("RC_PIPE_RES_CUS")) res = std::atoi(e);
-  p.lanes = 2;
-  p.slots = 4;
-  if (const char* e = std::getenv("RC_PIPE_RESOLVERS")) p.lanes = std::atoi(e);
+  if (tu.pipe_res_cus > 0) res = tu.pipe_res_cus;
+  p.lanes = tu.pipe_resolvers;
   if (p.lanes < 1) p.lanes = 1;
   if (p.lanes > Pipe::kLanes) p.lanes = Pipe::kLanes;
-  if (const char* e = std::getenv("RC_PIPE_SLOTS")) p.slots = std::atoi(e);
+  p.slots = tu.pipe_slots;
   if (p.slots < p.lanes + 1) p.slots = p.lanes + 1;
   if (p.slots > Pipe::kSlots) p.slots = Pipe::kSlots;
-  p.rt_on = !std::getenv("RC_PIPE_NO_RT");
-  p.fifo = !std::getenv("RC_PIPE_SLOTSTREAMS");
+  p.rt_on = tu.pipe_timing != 0;
+  p.fifo = tu.pipe_slotstreams == 0;
   res = res / (8 * p.lanes) * (8 * p.lanes);   // whole CUs per XCD for every resolver
   if (res < 16 * p.lanes) res = 16 * p.lanes;
   if (res > c.cus - 16) res = (c.cus - 16) / (8 * p.lanes) * (8 * p.lanes);
@@ -965,7 +1028,7 @@ int rc_render(const rc_scene* s, int W, int H, const rc_options* opt, uint8_t* p
   std::lock_guard<std::mutex> lk(c->mu);
   // parity: the copy overlaps the resolver (copy_overlapped); split shading leaves the non-DEP
   // colours to phase C, so its framebuffer is not final after phase A
-  const bool overlap = parity && !std::getenv("RC_SPLIT_SHADE") && !std::getenv("RC_SERIAL_D2H");
+  const bool overlap = parity && !tune().split_shade && tune().overlap_d2h;
   uint32_t* patch = nullptr;
   if (overlap) {
     if ((!c->d2h && hipStreamCreateWithFlags(&c->d2h, hipStreamNonBlocking) != hipSuccess) ||

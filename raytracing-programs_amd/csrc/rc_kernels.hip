@@ -2115,8 +2115,10 @@ int phase_c_side_blocks(int cus, int side_lds) {
           hipSuccess ||
       per_cu <= 0)
     per_cu = 1;
+#if RC_DIAG
   if (std::getenv("RC_SIDE_STATS"))
     std::fprintf(stderr, "side lds %d -> %d workgroups per CU\n", side_lds, per_cu);
+#endif
   return per_cu * cus;
 }
 

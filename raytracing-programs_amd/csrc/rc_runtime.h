@@ -131,6 +131,8 @@ struct DevCtx {
 
 extern DevCtx g_ctx[kMaxDevices];
 
+// process-wide schedule tuning (rc_set_tuning; defaults = the product's schedule)
+const rc_tuning& tune();
 int ctx_get(int device, DevCtx** out);
 int copy_to_host(DevCtx& c, uint8_t* host, const uint8_t* dev, size_t bytes, hipStream_t st);
 void prefault(uint8_t* p, size_t n);

@@ -5,6 +5,8 @@ import torch
 from helpers import golden_table, p3_md5, rc, scene_path
 n = int(os.environ.get("SIZE", "4096"))
 s = rc.Scene.from_file(scene_path(os.environ.get("SCENE", "quadric")))
+if os.environ.get("HELPERS"):   # schedule experiment (rc_set_tuning)
+    rc.set_tuning(helpers=int(os.environ["HELPERS"]))
 out = torch.empty((n, n, 3), dtype=torch.uint8, device="cuda")
 for _ in range(2):
     rc.render_device(s, n, n, out.data_ptr(), depth=6, mode="parity")

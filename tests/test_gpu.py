@@ -57,28 +57,34 @@ def test_configs(key, scenes, table):
     assert p3_md5(img) == table[key]["md5"], key
 
 
-@pytest.mark.parametrize("knob", ["RC_NO_SIDE", "RC_SPLIT_SHADE", "RC_RESOLVE_SHARED",
-                                  "RC_NO_DEP_FAST", "RC_NO_SIDE+RC_NO_DEP_FAST",
-                                  "RC_NO_SIDE+RC_PHASE_C_FINISH", "RC_NO_O0", "RC_HAND_RUN",
-                                  "RC_HELPERS"])
-def test_parity_schedules(knob, scenes, table, monkeypatch):
-    """The parity pipeline's alternative schedules give the same bytes: phase C after the
-    resolver only (RC_NO_SIDE: clean entries, then full waves of the rest — k_dep_chunks;
-    with RC_PHASE_C_FINISH through k_finish's batch claims), colours shaded
-    beside the resolver (RC_SPLIT_SHADE), and no one-workgroup-per-CU reservation
-    (RC_RESOLVE_SHARED, which also disables the side stream), and every first-bounce-miss
-    pixel recomputed in phase C (RC_NO_DEP_FAST), primary rays through the general
-    intersection tests instead of the origin-zero forms (RC_NO_O0), a hand-off to the helper
-    blocks after every change (RC_HAND_RUN=1: the queue overflows) and a single helper block
-    (RC_HELPERS=1)."""
-    for k in knob.split("+"):
-        monkeypatch.setenv(k, "1")
-    for key in ("quadric:4096x4096:d6:parity", "reflection:2048x2048:d4:parity",
-                "quadric:333x517:d6:parity"):
-        scene, size, d, mode = key.split(":")
-        w, h = map(int, size.split("x"))
-        img = rc.render(scenes[scene], w, h, depth=int(d[1:]), mode=mode)
-        assert p3_md5(img) == table[key]["md5"], (knob, key)
+SCHEDULES = {"no-side": dict(side=0), "split-shade": dict(split_shade=1),
+             "resolve-shared": dict(resolve_shared=1), "no-dep-fast": dict(dep_fast=0),
+             "no-side+no-dep-fast": dict(side=0, dep_fast=0),
+             "no-side+phase-c-finish": dict(side=0, phase_c_finish=1), "no-o0": dict(o0=0),
+             "hand-run-1": dict(hand_run=1), "helpers-1": dict(helpers=1),
+             "no-helpers": dict(helpers=0), "no-coop": dict(coop=0),
+             "small-grid": dict(resolve_grid=64, team_blocks=16),
+             "serial-plain-d2h": dict(overlap_d2h=0, staged_d2h=0, prefault=0)}
+
+
+@pytest.mark.parametrize("sched", list(SCHEDULES))
+def test_parity_schedules(sched, scenes, table):
+    """The parity pipeline's alternative schedules (rc_set_tuning) give the same bytes:
+    phase C after the resolver only (side=0: clean entries, then full waves of the rest —
+    k_dep_chunks; with phase_c_finish through k_finish's batch claims), colours shaded beside
+    the resolver (split_shade), no one-workgroup-per-CU reservation (resolve_shared, which
+    also disables the side stream), every first-bounce-miss pixel recomputed in phase C
+    (dep_fast=0), primary rays through the general intersection tests instead of the origin-
+    zero forms (o0=0), a hand-off to the helper blocks after every change (hand_run=1: the
+    queue overflows), a single helper block, none, the lane-only evaluator (coop=0), a small
+    resolver grid, and the plain serial copy to the host."""
+    with rc.tuned(**SCHEDULES[sched]):
+        for key in ("quadric:4096x4096:d6:parity", "reflection:2048x2048:d4:parity",
+                    "quadric:333x517:d6:parity"):
+            scene, size, d, mode = key.split(":")
+            w, h = map(int, size.split("x"))
+            img = rc.render(scenes[scene], w, h, depth=int(d[1:]), mode=mode)
+            assert p3_md5(img) == table[key]["md5"], (sched, key)
 
 
 @pytest.mark.parametrize("n_shapes", [20, 33, 64, 65, 90])
@@ -108,7 +114,7 @@ ZERO_EVENT_PLANES = [((0, 0, 1), 0.5, ""), ((0, 0.6, 0.8), 0.5, ""), ((0, 0.28, 
 @pytest.mark.parametrize("case", range(len(ZERO_EVENT_PLANES)))
 @pytest.mark.parametrize("fast_dep", [True, False])
 @pytest.mark.parametrize("side", [True, False])
-def test_zero_normalize_events(case, fast_dep, side, tmp_path, monkeypatch):
+def test_zero_normalize_events(case, fast_dep, side, tmp_path):
     """Zero-length normalize events (C/v3math.c:183-187; raycast() prints one stderr line per
     event): a point light exactly on the hit point of the 1x1 image's ray.  The pixel is a
     first-bounce miss; phase A counts its primary part and phase C the rest, with the clean-
@@ -121,17 +127,15 @@ def test_zero_normalize_events(case, fast_dep, side, tmp_path, monkeypatch):
                     + extra +
                     "light, color: [4, 4, 4], radial-a2: 0.01, radial-a1: 0.0125, "
                     "radial-a0: 0.0125, position: [0, 0, -5]\n")
-    if not fast_dep:
-        monkeypatch.setenv("RC_NO_DEP_FAST", "1")
-    if not side:   # phase C after the resolver: k_dep_chunks
-        monkeypatch.setenv("RC_NO_SIDE", "1")
     s = rc.Scene.from_file(str(path))
-    for w, h in ((1, 1), (2, 1), (3, 1), (1, 3)):
-        want, st = oracle_render(s, w, h, 6, "parity")
-        tim = {}
-        got = rc.render(s, w, h, depth=6, mode="parity", timing=tim)
-        np.testing.assert_array_equal(got, want, err_msg=f"{w}x{h}")
-        assert tim["zero_normalize"] == st["zero_normalize"], (w, h, tim, st["zero_normalize"])
+    # side=0: phase C after the resolver (k_dep_chunks)
+    with rc.tuned(dep_fast=int(fast_dep), side=int(side)):
+        for w, h in ((1, 1), (2, 1), (3, 1), (1, 3)):
+            want, st = oracle_render(s, w, h, 6, "parity")
+            tim = {}
+            got = rc.render(s, w, h, depth=6, mode="parity", timing=tim)
+            np.testing.assert_array_equal(got, want, err_msg=f"{w}x{h}")
+            assert tim["zero_normalize"] == st["zero_normalize"], (w, h, tim, st["zero_normalize"])
     assert oracle_render(s, 1, 1, 6, "parity")[1]["zero_normalize"] > 0
 
 
@@ -219,22 +223,21 @@ def test_device_render_matches_host(scenes, table):
 
 
 PIPES = {"default": {},
-         "slot-streams": {"RC_PIPE_SLOTSTREAMS": "1"},
-         "three-lanes": {"RC_PIPE_RESOLVERS": "3", "RC_PIPE_RES_CUS": "144", "RC_PIPE_SLOTS": "6"},
-         "one-lane-small-a": {"RC_PIPE_RESOLVERS": "1", "RC_PIPE_RES_CUS": "32",
-                              "RC_PIPE_NO_RT": "1"},
-         "one-wg-per-cu": {"RC_RESOLVE_LDS_KB": "96", "RC_TEAM_BLOCKS": "24"}}
+         "slot-streams": dict(pipe_slotstreams=1),
+         "three-lanes": dict(pipe_resolvers=3, pipe_res_cus=144, pipe_slots=6),
+         "one-lane-small-a": dict(pipe_resolvers=1, pipe_res_cus=32, pipe_timing=0),
+         "one-wg-per-cu": dict(resolve_lds_kb=96, team_blocks=24)}
 
 
 @pytest.mark.parametrize("pipe", list(PIPES))
-def test_frames_in_flight(pipe, scenes, table, monkeypatch):
+def test_frames_in_flight(pipe, scenes, table):
     """rc_frame_submit: consecutive frames overlap on two CU partitions (the resolver of one
     beside the pixel phases of the next); every frame is still byte-identical.  Mixed scenes,
     sizes and modes exercise the slot workspaces' re-use and re-upload; the pipeline is
     rebuilt (rc_pipe_reset) under each partition / stream layout."""
     torch = pytest.importorskip("torch")
-    for k, v in PIPES[pipe].items():
-        monkeypatch.setenv(k, v)
+    saved = rc.get_tuning()
+    rc.set_tuning(**PIPES[pipe])
     rc.pipe_reset()
     seq = ["quadric:4096x4096:d6:parity", "reflection:2048x2048:d4:parity",
            "quadric:4096x4096:d6:parity", "simple:1024x1024:d6:parity",
@@ -255,10 +258,10 @@ def test_frames_in_flight(pipe, scenes, table, monkeypatch):
             rc.frame_submit(scenes[scene], w, h, buf.data_ptr(), depth=d, mode=mode)
         tim = {}
         rc.frames_wait(tim)
-        assert tim["resolve_ms"] > 0.0 or "RC_PIPE_NO_RT" in PIPES[pipe]
+        assert tim["resolve_ms"] > 0.0 or PIPES[pipe].get("pipe_timing") == 0
         for key, scene, w, h, d, mode, buf in jobs:
             assert p3_md5(buf.cpu().numpy()) == table[key]["md5"], (pipe, key)
-    monkeypatch.undo()
+    rc.set_tuning(**saved)
     rc.pipe_reset()   # later tests get the default pipeline
 
 
