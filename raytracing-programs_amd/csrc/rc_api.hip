@@ -1077,6 +1077,19 @@ static void consume_lists(json_data_t* js) {
 void raycast(json_data_t* json_struct, PPMFormat photo_data) {
   rc_options opt;
   rc_default_options(&opt, 1);
+  // The reference's main mallocs json_struct and zeroes num_shapes but not num_lights
+  // (C/raycast.c:41-44): it relies on a fresh, zeroed heap chunk.  Linked against this library
+  // the heap has been used before main (the HIP runtime), so the count can be garbage.  A count
+  // above the list's length (which the reference would walk off the end of) or below zero is
+  // taken as the list's length — what the zeroed chunk gives the reference — and written back,
+  // so main's own report of the counts (C/raycast.c:66-67) is right too.
+  {
+    int ns = 0, nl = 0;
+    for (const shape_t* p = json_struct->shapes_list; p; p = p->next) ++ns;
+    for (const light_t* p = json_struct->lights_list; p; p = p->next) ++nl;
+    if (json_struct->num_shapes < 0 || json_struct->num_shapes > ns) json_struct->num_shapes = ns;
+    if (json_struct->num_lights < 0 || json_struct->num_lights > nl) json_struct->num_lights = nl;
+  }
   rc_scene* s = rc_scene_create(json_struct);
   if (!s) {
     std::fprintf(stderr, "Error: could not flatten the scene lists\n");

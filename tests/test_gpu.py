@@ -192,13 +192,14 @@ def test_option_b_reference_main(tmp_path, table):
     """INTEGRATION.md Option B: the reference's own program (C/raycast.c:19-69 main, its own
     parse.c / ppm.c) with its raycast() fenced off by #ifndef RAYCAST_HIP (oracle/Makefile),
     linked against libraycast_hip.so: C1 and C4 files md5-equal to the reference's."""
-    for scene, n, key in [("simple", 256, "simple:256x256:d6:parity"),
-                          ("quadric", 4096, "quadric:4096x4096:d6:parity")]:
+    for scene, n, key, counts in [("simple", 256, "simple:256x256:d6:parity", (4, 1)),
+                                  ("quadric", 4096, "quadric:4096x4096:d6:parity", (5, 2))]:
         out = tmp_path / f"{scene}.ppm"
         r = subprocess.run([OPTB, str(n), str(n), scene_path(scene), str(out)],
                            capture_output=True, text=True, timeout=300)
         assert r.returncode == 0, r.stderr
-        assert "image with" in r.stdout
+        # main's own report; its num_lights starts uninitialised (C/raycast.c:41-44)
+        assert f"image with {counts[0]} shape(s) and {counts[1]} light(s)" in r.stdout, r.stdout
         assert file_md5(str(out)) == table[key]["md5"], key
 
 
