@@ -14,6 +14,7 @@ name has a hyphen; ``__graft_entry__`` and tests load it by path).
 """
 import ctypes
 import os
+import sys
 
 import numpy as np
 
@@ -129,8 +130,25 @@ def front_lib():
     return lib
 
 
+def _one_hip_runtime():
+    """PyTorch-ROCm bundles its own HIP runtime (torch/lib/libamdhip64.so, SONAME
+    libamdhip64.so.7, which torch's libraries reference as plain `libamdhip64.so`).  If
+    libraycast_hip.so loaded /opt/rocm's runtime first and torch were imported later, the
+    loader would map a second HIP runtime into the process (two device contexts; their
+    teardown corrupts the heap at exit).  Importing torch first makes libraycast_hip.so's
+    `libamdhip64.so.7` / `librccl.so.1` resolve to the runtime already loaded: one per
+    process.  Without torch, /opt/rocm's runtime is the only one."""
+    if "torch" in sys.modules:
+        return
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+
+
 def hip_lib():
     # RC_HIP_LIB selects a diagnostic build (e.g. libraycast_hip_stamps.so); never the default
+    _one_hip_runtime()
     lib = _load(os.environ.get("RC_HIP_LIB", "libraycast_hip.so"))
     lib.rc_scene_create.argtypes = [ctypes.POINTER(JsonDataT)]
     lib.rc_scene_create.restype = ctypes.c_void_p
