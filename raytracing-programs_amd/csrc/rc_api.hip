@@ -467,9 +467,13 @@ int ensure_parity(DevCtx& c, FrameBufs& b, int W, int H, rc::ParityWork& w, int 
   if (tu.resolve_grid >= 8 && tu.resolve_grid < w.resolve_blocks)   // experiments: a smaller grid
     w.resolve_blocks = tu.resolve_grid;
   w.resolve_lds = c.resident_lds;
-  // team size: 128 of a whole-device grid; 3/8 of a pipelined resolver's grid (64 -> 24:
-  // measured 4.77e9 vs 4.50e9 rays/s at 32, 4.49e9 at 20)
-  w.team_blocks = piped ? w.resolve_blocks * 3 / 8 : 128;
+  // team size: 128 of a whole-device grid.  A pipelined resolver's grid: half of it for the
+  // 8-32 Mpixel images, whose resolver lanes hold half the device (quadric 4096^2: 5.70e9 ->
+  // 5.87e9 rays/s at 64 of 128, 5.82e9 at 56, 5.45e9 at 80: a larger team scans the 707k-entry
+  // clean stretch in fewer rounds), 3/8 otherwise (reflection 2048^2 d4 7.6e9 vs 7.4e9 at half,
+  // simple 1024^2 d6 3.1e9 vs 2.9e9; quadric 8192^2 unchanged, its resolvers slower at half)
+  const bool half_team = P >= ((size_t)8 << 20) && P < ((size_t)32 << 20);
+  w.team_blocks = !piped ? 128 : half_team ? w.resolve_blocks / 2 : w.resolve_blocks * 3 / 8;
   if (tu.team_blocks >= 0) w.team_blocks = tu.team_blocks;
   if (w.team_blocks > 256) w.team_blocks = 256;
   if (w.team_blocks > w.resolve_blocks / 2) w.team_blocks = w.resolve_blocks / 2;
