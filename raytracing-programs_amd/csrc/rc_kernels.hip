@@ -882,7 +882,12 @@ __device__ __forceinline__ void block_window(const Scene& sc, int maxrec, BlockW
       const DepRec ri = bw.rec[i];
       V3 oc = ce;
       bool hg = false;
+#if RC_STAMPS
+      Stamps stp = {{0, 0, 0, 0}, 0};
+#define RC_SPEC1(GT, Q) carry_path_spec<GT, Q>(sc, ls, kself, G, half, ri, maxrec, ce, zero, hg, &stp)
+#else
 #define RC_SPEC1(GT, Q) carry_path_spec<GT, Q>(sc, ls, kself, G, half, ri, maxrec, ce, zero, hg)
+#endif
 #define RC_SPEC(GT) (sc.has_quadric ? RC_SPEC1(GT, true) : RC_SPEC1(GT, false))
       if (G == 8) oc = RC_SPEC(8);
       else if (G == 4) oc = RC_SPEC(4);
