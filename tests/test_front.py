@@ -209,3 +209,22 @@ def test_option_b_links_library(tmp_path):
         r = subprocess.run([OPTB, "8", "8", scene_path("quadric"), str(tmp_path / "o.ppm")],
                            capture_output=True, text=True, timeout=60)
         assert "could not flatten" not in r.stderr, r.stderr
+
+
+def test_tuning_api_validates():
+    """rc_set_tuning (the explicit replacement for environment knobs) rejects out-of-range
+    fields without changing anything and round-trips valid ones; no GPU is touched."""
+    base = rc.get_tuning(default=True)
+    assert rc.get_tuning() == base
+    for bad in (dict(pipe_resolvers=0), dict(pipe_resolvers=5), dict(helpers=65),
+                dict(team_blocks=-2), dict(resolve_grid=4), dict(split_shade=1, side=0),
+                dict(copy_threads=0), dict(resolve_lds_kb=200), dict(long_len=10)):
+        with pytest.raises(ValueError):
+            rc.set_tuning(**bad)
+        assert rc.get_tuning() == base, bad
+    with rc.tuned(side=0, helpers=1, team_blocks=24):
+        t = rc.get_tuning()
+        assert (t["side"], t["helpers"], t["team_blocks"]) == (0, 1, 24)
+    assert rc.get_tuning() == base
+    with pytest.raises(KeyError):
+        rc.set_tuning(no_such_field=1)
