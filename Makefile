@@ -98,3 +98,15 @@ $(SAN_OUT)/oracle_raytrace: oracle/oracle_main.c oracle/rc_oracle.c oracle/rc_or
 $(SAN_OUT)/front_check: tests/tools/front_check.c $(FRONT_SRC) include/raycast_hip.h
 	@mkdir -p $(SAN_OUT)
 	$(CC) -O1 -ffp-contract=off $(SAN) -Iinclude -I$(SRC) tests/tools/front_check.c $(FRONT_SRC) -o $@ -lm -lpthread
+
+# occupancy variants of the pixel kernels (RC_HIP_LIB=libraycast_hip_<v>.so): w3 = phase A /
+# k_render compiled for 3 waves per SIMD (no VGPR spills), f3 = phase C (k_dep_chunks, k_finish)
+occupancy: $(LIB)/libraycast_hip_w3.so $(LIB)/libraycast_hip_f3.so $(LIB)/libraycast_hip_c512.so $(LIB)/libraycast_hip_c2048.so
+$(OBJ)/c512_kernels.o: $(SRC)/rc_kernels.hip $(HIP_HDRS)
+	$(HIPCC) $(HIPFLAGS) -DRC_CHUNK=512 -c $< -o $@
+$(OBJ)/c2048_kernels.o: $(SRC)/rc_kernels.hip $(HIP_HDRS)
+	$(HIPCC) $(HIPFLAGS) -DRC_CHUNK=2048 -c $< -o $@
+$(OBJ)/w3_kernels.o: $(SRC)/rc_kernels.hip $(HIP_HDRS)
+	$(HIPCC) $(HIPFLAGS) -DRC_PHASE_A_WAVES=3 -c $< -o $@
+$(OBJ)/f3_kernels.o: $(SRC)/rc_kernels.hip $(HIP_HDRS)
+	$(HIPCC) $(HIPFLAGS) -DRC_FINISH_WAVES=3 -c $< -o $@

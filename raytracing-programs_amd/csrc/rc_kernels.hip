@@ -1695,7 +1695,10 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_
 // is not dep_fast).  Entries are independent once their carry-ins are known, so the list order
 // is free; the point is full waves of heavy work (~35 % of the entries are clean at quadric
 // 4096^2) without a second kernel or global atomics.
-constexpr int kChunk = 1024;
+#ifndef RC_CHUNK
+#define RC_CHUNK 1024
+#endif
+constexpr int kChunk = RC_CHUNK;
 
 template <bool kStage>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_FINISH_WAVES))) k_dep_chunks(
