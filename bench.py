@@ -68,20 +68,27 @@ def load_pkg():
     return mod
 
 
-def pmc_traffic(kernel, scene, size, depth, mode):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of this
-    exact configuration (profiles/r01_pmc_traffic_<size>.json: 2*FETCH_SIZE + WRITE_SIZE, the
-    gfx950 correction of MI355X_MICROARCH.md); None when no profile covers it."""
-    path = os.path.join(ROOT, "profiles", f"r01_pmc_traffic_{size}.json")
-    if scene != "quadric" or depth != 6 or not os.path.exists(path):
+# rocprofv3 --pmc summaries of this exact configuration from HEAD (scripts/pmc_valu.sh,
+# scripts/pmc_fast.sh -> scripts/pmc_summary.py): per-kernel counter means per launch.
+PMC_PROFILES = {("quadric", 4096, 6, "parity"): "profiles/r02b_pmc_lone_4096.json",
+                ("quadric", 4096, 6, "fast"): "profiles/r02b_pmc_fast_4096.json"}
+
+
+def pmc_kernel(kernel, scene, size, depth, mode):
+    """Counter means of `kernel` from the committed PMC summary of this configuration:
+    hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 per launch (the gfx950 correction of
+    MI355X_MICROARCH.md), write_bytes = WRITE_SIZE * 1024, valu_busy; (None, None) when no
+    profile covers it."""
+    rel = PMC_PROFILES.get((scene, size, depth, mode))
+    if not rel or not os.path.exists(os.path.join(ROOT, rel)):
         return None, None
-    with open(path) as f:
+    with open(os.path.join(ROOT, rel)) as f:
         prof = json.load(f)
-    if mode not in prof.get("config", ""):
-        return None, None
     for name, d in prof["kernels"].items():
-        if name.split("::")[-1].split("<")[0] == kernel and "hbm_bytes" in d:
-            return d["hbm_bytes"], os.path.relpath(path, ROOT)
+        if name.split("::")[-1].split("<")[0] == kernel:
+            return {"hbm_bytes": d.get("hbm_bytes"),
+                    "write_bytes": d["WRITE_SIZE"] * 1024 if "WRITE_SIZE" in d else None,
+                    "valu_busy": d.get("valu_busy")}, rel
     return None, None
 
 
@@ -360,7 +367,10 @@ def main():
         # per step: the dominant kernel's algorithmic work of one image over the step time
         # (with frames in flight two resolvers overlap, so per-launch and per-step differ)
         ach_step = (dom_flop * images / world) / (step_ms * 1e-3) / 1e12 if dom_flop else None
-        traffic, traffic_src = pmc_traffic(dom_name, args.scene, args.size, args.depth, mode)
+        pmc, pmc_src = pmc_kernel(dom_name, args.scene, args.size, args.depth, mode)
+        store_name = "k_phase_a" if parity else "k_render"   # the framebuffer's writer
+        spmc, _ = pmc_kernel(store_name, args.scene, args.size, args.depth, mode)
+        store_ms = phases["phase_a_ms"] if parity else phases["render_ms"]
         rach = (work["render_flop_per_px"] * W * rows_here / (render_ms * 1e-3) / 1e12
                 if work and render_ms else None)
         line = {
@@ -397,9 +407,10 @@ def main():
                          "frac": round(ach / PEAK_FP64_TFLOPS, 5) if ach else None,
                          "achieved_per_step": round(ach_step, 4) if ach_step else None,
                          "frac_per_step": round(ach_step / PEAK_FP64_TFLOPS, 5) if ach_step else None,
-                         "traffic": traffic,
+                         "traffic": pmc["hbm_bytes"] if pmc else None,
                          "traffic_unit": "bytes per launch (HBM, PMC)",
-                         "traffic_source": traffic_src,
+                         "valu_busy": pmc["valu_busy"] if pmc else None,
+                         "pmc_source": pmc_src,
                          "note": ("serial carry chain: latency-bound, see DESIGN.md; frac = per "
                                   "launch, frac_per_step = one image's work over ms_per_step"
                                   if parity else "throughput kernel")},
@@ -409,10 +420,17 @@ def main():
                                 "achieved": round(rach, 3) if rach else None,
                                 "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
                                 "frac": round(rach / PEAK_FP64_TFLOPS, 4) if rach else None},
-            "roofline_hbm": {"bound": "hbm", "kernel": "framebuffer store (3 B/pixel)",
-                             "achieved": round(3 * W * rows_here / (phases["total_ms"] * 1e-3) / 1e9, 3)
-                             if phases.get("total_ms") else None,
-                             "peak": PEAK_HBM_GBS, "unit": "GB/s"},
+            # the framebuffer store: its writer kernel's HBM write bytes (PMC WRITE_SIZE, which
+            # for phase A also holds the classes, writer carries and DEP records) over that
+            # kernel's time; the algorithmic 3 B/pixel beside it
+            "roofline_hbm": {"bound": "hbm", "kernel": store_name + " (framebuffer store)",
+                             "achieved": (round(spmc["write_bytes"] / (store_ms * 1e-3) / 1e9, 3)
+                                          if spmc and spmc.get("write_bytes") and store_ms
+                                          else None),
+                             "algorithmic": (round(3 * W * rows_here / (store_ms * 1e-3) / 1e9, 3)
+                                             if store_ms else None),
+                             "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                             "write_bytes_pmc": spmc["write_bytes"] if spmc else None},
         }
         if single:
             line["single_frame"] = single
