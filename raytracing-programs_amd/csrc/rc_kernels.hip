@@ -774,6 +774,64 @@ __device__ __forceinline__ void cin_put(CinG* cin, int j, V3 c, unsigned tag, bo
   __hip_atomic_store(&cin[j].g[2], pack2(__float_as_uint(c.z), tg), __ATOMIC_RELAXED,
                      __HIP_MEMORY_SCOPE_AGENT);
 }
+// A whole wave publishes the entries j0+lo .. j0+hi-1 (lanes lo..hi-1 of the wave's 64-entry
+// slice) together: store instruction i writes granule 64*i + lane of the slice, so each
+// instruction covers 512 contiguous bytes instead of 64 granules at a 24-byte stride (the
+// agent-scope stores write through to memory: strided granules cost ~3x their bytes in HBM
+// writes, rocprofv3 WRITE_SIZE).  Every granule is still one 8-byte atomic store with its own
+// tag, so readers are unchanged.  The carry is either the wave's own per-lane value
+// (cin_put_wave) or one carry for the whole range (cin_put_wave_uniform); hitmask bit e is
+// entry lane e's hit flag.  Every lane of the wave must call these.
+__device__ __forceinline__ void cin_put_granules(CinG* cin, int j0, int lo, int hi, V3 c_lane,
+                                                 bool uniform, unsigned tag,
+                                                 unsigned long long hitmask) {
+  const int lane = threadIdx.x & 63;
+  unsigned long long* g = &cin[j0].g[0];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int q = 64 * i + lane;
+    const int e = q / 3, comp = q - 3 * e;
+    float x = c_lane.x, y = c_lane.y, z = c_lane.z;
+    if (!uniform) {
+      x = __shfl(x, e, 64);
+      y = __shfl(y, e, 64);
+      z = __shfl(z, e, 64);
+    }
+    const float v = comp == 0 ? x : (comp == 1 ? y : z);
+    const unsigned tg = tag | (((hitmask >> e) & 1ull) ? kCinHit : 0u);
+    if (e >= lo && e < hi)
+      __hip_atomic_store(&g[q], pack2(__float_as_uint(v), tg), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+// Per-lane carries staged through the wave's own 768 bytes of LDS (entry-major x, y, z: float
+// q of the stage is granule q's value) instead of cross-lane shuffles.
+__device__ __forceinline__ void cin_put_wave(CinG* cin, int j0, int lo, int hi, V3 c_lane,
+                                             unsigned tag, unsigned long long hitmask,
+                                             float* stage) {
+  const int lane = threadIdx.x & 63;
+  stage[3 * lane] = c_lane.x;
+  stage[3 * lane + 1] = c_lane.y;
+  stage[3 * lane + 2] = c_lane.z;
+  __builtin_amdgcn_wave_barrier();   // one wave's LDS accesses complete in order
+  unsigned long long* g = &cin[j0].g[0];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int q = 64 * i + lane;
+    const int e = q / 3;
+    const unsigned tg = tag | (((hitmask >> e) & 1ull) ? kCinHit : 0u);
+    const float v = stage[q];
+    if (e >= lo && e < hi)
+      __hip_atomic_store(&g[q], pack2(__float_as_uint(v), tg), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __builtin_amdgcn_wave_barrier();   // the stage is rewritten by the next window
+}
+__device__ __forceinline__ void cin_put_wave_uniform(CinG* cin, int j0, int lo, int hi, V3 c,
+                                                     unsigned tag, unsigned long long hitmask) {
+  cin_put_granules(cin, j0, lo, hi, c, true, tag, hitmask);
+}
+
 __device__ __forceinline__ bool cin_get(CinG* cin, int j, unsigned tag, V3& c, bool& hit) {
   const unsigned long long a =
       __hip_atomic_load(&cin[j].g[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1009,7 +1067,13 @@ __device__ __forceinline__ void block_window(const Scene& sc, int maxrec, BlockW
     } else {
       last = coop ? (pos + Eb < nvalid ? pos + Eb : nvalid) - 1 : nvalid - 1;
     }
-    if (t >= pos && t <= last) cin_put(cin, base + t, c, tag, bw.hit[t] != 0);
+    {   // entries pos..last of this window read carry c: each wave publishes its 64-entry slice
+      const int w0 = wave * 64;
+      const int lo = pos - w0 > 0 ? pos - w0 : 0;
+      const int hi = last + 1 - w0 < 64 ? last + 1 - w0 : 64;
+      const unsigned long long hm = __ballot(bw.hit[t] != 0);
+      if (lo < hi) cin_put_wave_uniform(cin, base + w0, lo, hi, c, tag, hm);
+    }
     if (hp) {   // keep the predictor's history across the non-predictive steps
       if (!hit || last > pos) hp->n = 0;
       if (hit) {
@@ -1261,7 +1325,14 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
           __syncthreads();
           const int gpos = s_gpos;
           // entries before the first changer, and the changer itself, read carry c
-          if (valid && idx <= gpos) cin_put(cin, idx, c, tag, h);
+          {
+            // entries up to the first changer (gpos = 0x7fffffff: none in this round)
+            const long long hi0 = end - base < 64 ? end - base : 64;
+            const long long hi1 = (long long)gpos - base + 1;
+            const int hi = (int)(hi1 < hi0 ? hi1 : hi0);
+            const unsigned long long hm = __ballot(valid && h);
+            if (hi > 0) cin_put_wave_uniform(cin, base, 0, hi, c, tag, hm);
+          }
           if (gpos == 0x7fffffff) {
             j += window;
           } else {
@@ -1438,7 +1509,13 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
                            , &stp
 #endif
                            );
-      if (j + lane < end) cin_put(cin, j + lane, mine, tag, mhit);
+      {
+        // the block-window LDS is free in the regular loop (team and helper work is over):
+        // 768 bytes per wave stage the publication
+        const unsigned long long hm = __ballot(j + lane < end && mhit);
+        cin_put_wave(cin, j, 0, end - j < 64 ? end - j : 64, mine, tag, hm,
+                     reinterpret_cast<float*>(&s_bw) + wave * 192);
+      }
       // a long run of changers: hand the rest of the segment to a helper block (15 carry
       // guesses per step instead of this wave's 3)
       if (helpers > 0 && hs.run >= hand_run && hs.n >= 2 && end - (j + 64) >= kHandMin) {
