@@ -574,6 +574,11 @@ __device__ __forceinline__ void shoot(const Scene& sc, V3 d, int maxrec, V3 carr
   if (i0 < 0) return;                                   // C/raycast.c:328-331
   V3 P0, N0;
   hit_frame(sc, i0, v3(0.0f, 0.0f, 0.0f), d, t0, P0, N0, zp);
+  // The primary hit's shade is added last (C/raycast.c:377-378) but depends on the primary hit
+  // alone: shading it first is the same arithmetic, added in the same order at the end, and
+  // P0 / N0 / d need not stay live through the bounce loop (register pressure: phase A spills).
+  V3 prim = v3(0.0f, 0.0f, 0.0f);
+  if (MODE != kModeClassify) prim = shade(sc, i0, P0, N0, d, zp);
 
   int obj = i0, S = i0;
   V3 O = P0, D = d, N = N0, C = carry;
@@ -599,7 +604,7 @@ __device__ __forceinline__ void shoot(const Scene& sc, V3 d, int maxrec, V3 carr
         const V3 A = normalize_sel(reflect(D, N));
         const V3 B = normalize_sel(reflect(A, N));
         po.dep = DepRec{A.x, A.y, A.z, N.x, N.y, N.z, obj, 0, B.x, B.y, B.z, 0};
-        if (MODE == kModeParityA && sc.dep_fast) po.pcol = shade(sc, i0, P0, N0, d, zp);
+        if (MODE == kModeParityA && sc.dep_fast) po.pcol = prim;
         zero_events += zp;
         return;
       }
@@ -614,10 +619,8 @@ __device__ __forceinline__ void shoot(const Scene& sc, V3 d, int maxrec, V3 carr
     O = C;
     S = i;
   }
-  if (MODE != kModeClassify) {
-    V3 col = shade(sc, i0, P0, N0, d, zp);             // C/raycast.c:377-378
-    out = v3(out.x + col.x, out.y + col.y, out.z + col.z);
-  }
+  if (MODE != kModeClassify)                            // C/raycast.c:377-378
+    out = v3(out.x + prim.x, out.y + prim.y, out.z + prim.z);
   zero_events += zp;
   po.rgb = out;
   po.cls = wrote ? kClsWriter : kClsIdent;
@@ -629,8 +632,10 @@ __device__ __forceinline__ void shoot(const Scene& sc, V3 d, int maxrec, V3 carr
 // computed (pcol, C/raycast.c:377-378).  Level 1 missed: its shade is the black phantom's
 // (exactly zero), O = C = c, S = -1, N = N0, obj = obj0, T = refl[obj0]^2, and level 2's
 // direction normalize(reflect(D1, N0)) is the record's `a`.
+// The primary shade is read after the bounce loop (pcol: phase A's slot of the pixel), so it
+// does not stay live through it (register pressure: phase C spills).
 __device__ __forceinline__ V3 shade_dep_cont(const Scene& sc, const DepRec& r, int maxrec, V3 c,
-                                             V3 pcol, int& zero_events) {
+                                             const float4* __restrict__ pcol, int& zero_events) {
   int obj = r.obj0, S = -1;
   const float T0 = sc.lshapes[obj].refl;
   float T = T0 * sc.lshapes[obj].refl;
@@ -653,7 +658,8 @@ __device__ __forceinline__ V3 shade_dep_cont(const Scene& sc, const DepRec& r, i
     O = C;
     S = i;
   }
-  return v3(out.x + pcol.x, out.y + pcol.y, out.z + pcol.z);
+  const float4 k = *pcol;
+  return v3(out.x + k.x, out.y + k.y, out.z + k.z);
 }
 
 // Carry-only continuation of a DEP pixel from carry-in c (levels 2..maxrec-1): the

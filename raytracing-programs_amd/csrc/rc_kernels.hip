@@ -1620,9 +1620,14 @@ __device__ __forceinline__ void shade_batch(const Scene& sc, const Cam& cam, int
   if (j >= ndep) return;
   const long long p = dep_pix[j];
   if (sc.dep_fast) {
-    const float4 k = pcol[p];
-    const V3 pc = v3(k.x, k.y, k.z);
-    store_dep(out, patch, p, j, hit ? shade_dep_cont(sc, deprec[p], maxrec, c, pc, zero) : pc);
+    V3 rgb;
+    if (hit) {
+      rgb = shade_dep_cont(sc, deprec[p], maxrec, c, pcol + p, zero);
+    } else {
+      const float4 k = pcol[p];
+      rgb = v3(k.x, k.y, k.z);
+    }
+    store_dep(out, patch, p, j, rgb);
     return;
   }
   const int y = (int)(p / W), x = (int)(p % W);
@@ -1777,7 +1782,9 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_
 #endif
 constexpr int kChunk = RC_CHUNK;
 
-template <bool kStage>
+// kFast = Scene::dep_fast (host-known): each form compiles only its own shading path, which
+// keeps the other's live state out of the register budget.
+template <bool kStage, bool kFast>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_FINISH_WAVES))) k_dep_chunks(
     Scene sc, Cam cam, int W, int row0, int row_step, int maxrec,
     const long long* __restrict__ dep_pix,
@@ -1804,7 +1811,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_
       bool hit = true;
       (void)batch_carries(cin, ndep, b, tag, true, c, hit, ts);
       const bool in = j < ndep;
-      const bool hv = in && (!sc.dep_fast || hit);
+      const bool hv = in && (!kFast || hit);
       if (in && !hv) {
         const long long p = dep_pix[j];
         const float4 k = pcol[p];
@@ -1829,9 +1836,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_
       const V3 c = v3(s_c[q][0], s_c[q][1], s_c[q][2]);
       const long long p = dep_pix[j];
       V3 rgb;
-      if (sc.dep_fast) {
-        const float4 k = pcol[p];
-        rgb = shade_dep_cont(sc, deprec[p], maxrec, c, v3(k.x, k.y, k.z), zero);
+      if constexpr (kFast) {
+        rgb = shade_dep_cont(sc, deprec[p], maxrec, c, pcol + p, zero);
       } else {
         const int y = row0 + (int)(p / W) * row_step, x = (int)(p % W);   // p: local pixel
         const V3 d = primary_dir(cam, x, y, zero);
@@ -2160,7 +2166,8 @@ static void enqueue_phase_c(const Scene& sc, const Cam& cam, bool st, int W, int
                        out, w.patch,
                        zcount, (TeamState*)w.team, w.epoch, (w.side && w.split_shade) ? 1 : 0);
   } else {   // all of phase C after the resolver: clean entries, then full waves of the rest
-    hipLaunchKernelGGL(st ? k_dep_chunks<true> : k_dep_chunks<false>, dim3(w.phase_c_blocks),
+    hipLaunchKernelGGL((sc.dep_fast ? (st ? k_dep_chunks<true, true> : k_dep_chunks<false, true>)
+                               : (st ? k_dep_chunks<true, false> : k_dep_chunks<false, false>)), dim3(w.phase_c_blocks),
                        dim3(kBlock), 0, stream, sc, cam, W, 0, 1, maxrec, w.dep_pix,
                        (const DepRec*)w.deprec, (const float4*)w.wcarry, (CinG*)w.cin,
                        w.counters, out, w.patch, zcount, (TeamState*)w.team, w.epoch);
@@ -2297,7 +2304,8 @@ hipError_t launch_shard_phase_c(const LaunchScene& s, int W, int H, int row0, in
                                 unsigned long long* zcount, hipStream_t stream) {
   const Scene sc = make_scene(s);
   const Cam cam = make_cam(s, W, H);
-  hipLaunchKernelGGL(stage_fits(s) ? k_dep_chunks<true> : k_dep_chunks<false>,
+  hipLaunchKernelGGL((s.dep_fast ? (stage_fits(s) ? k_dep_chunks<true, true> : k_dep_chunks<false, true>)
+                                  : (stage_fits(s) ? k_dep_chunks<true, false> : k_dep_chunks<false, false>)),
                      dim3(w.phase_c_blocks), dim3(kBlock), 0, stream, sc, cam, W, row0, row_step,
                      maxrec, w.dep_pix, (const DepRec*)w.deprec, (const float4*)w.wcarry,
                      (CinG*)w.cin, w.counters, out, (uint32_t*)nullptr, zcount,
