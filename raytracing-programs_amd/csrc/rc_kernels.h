@@ -65,6 +65,7 @@ struct ParityWork {
   hipEvent_t rready, rdone; // main -> rstream after compaction; rstream -> pstream after it
   hipEvent_t rt0, rt1;      // optional: resolver start / end on rstream
   hipEvent_t adone;         // optional: recorded after phase A (pipelined phase A order)
+  hipStream_t cstream;      // optional (with adone): compaction on this stream after adone
   uint32_t* patch;          // optional [P] packed RGB of DEP entry j (rc_render's overlapped copy)
   int defer_c;              // pipelined: launch_parity stops after the resolver; phase C is
                             // enqueued later by launch_phase_c (after rdone)

@@ -2095,6 +2095,13 @@ hipError_t launch_parity(const LaunchScene& s, int W, int H, int maxrec, uint8_t
                        w.cls, w.wcarry, (DepRec*)w.deprec, zcount);
   if (ev) (void)hipEventRecord(ev[0], stream);
   if (w.adone) (void)hipEventRecord(w.adone, stream);
+  // frames in flight: the compaction (small latency-bound kernels that gate this frame's
+  // resolver) leaves the pixel partition, where its workgroups would queue behind the other
+  // frames' phase A / phase C workgroups
+  if (w.cstream && w.adone) {
+    (void)hipStreamWaitEvent(w.cstream, w.adone, 0);
+    stream = w.cstream;
+  }
   (void)hipMemsetAsync(w.counters, 0, 16 * sizeof(int), stream);   // nseg, head, ndep, ...
   (void)hipMemsetAsync(w.team, 0, sizeof(TeamState), stream);     // error + round tags
   const int row_blocks = (H + kRowWaves - 1) / kRowWaves;

@@ -73,6 +73,7 @@ struct Pipe {
   int lanes = 2;                     // resolver streams in use (RC_PIPE_RESOLVERS)
   int slots = 4;                     // workspaces / pixel streams in use (RC_PIPE_SLOTS)
   hipStream_t pix[kSlots] = {}, res[kLanes] = {};
+  hipStream_t comp[2] = {};          // compaction: no CU mask, highest priority (comp_stream)
   hipEvent_t ready[kSlots] = {}, done[kSlots] = {};
   bool fifo = true;                  // pa = pix[0] + pc[] (false: RC_PIPE_SLOTSTREAMS)
   hipStream_t pc[kLanes] = {};
