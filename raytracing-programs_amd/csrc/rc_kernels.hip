@@ -1709,16 +1709,19 @@ __global__ void __launch_bounds__(kSideBlock) k_side(
   __shared__ int s_go;
   __shared__ StageBuf<kStage> stage;
   stage_scene<kStage>(sc, stage);
-  // The grid is sized so that a resolver workgroup always fits beside k_side's workgroups on
-  // a CU (phase_c_side_blocks), so waiting here for every resolver workgroup to be resident
-  // cannot hold one out; the wait is bounded anyway (20 ms, then this workgroup leaves its
-  // work to k_finish).
+  // k_side's LDS reservation keeps it off CUs that hold a resolver workgroup
+  // (side_lds_bytes), so a k_side workgroup dispatched BEFORE the resolver's last workgroups
+  // holds a CU those need.  Each k_side workgroup therefore waits only briefly for the
+  // resolver's census (every resolver workgroup resident): normally a few microseconds; if
+  // the side stream won the dispatch race (seen on a process's first frame: the resolver then
+  // took 24 ms behind a 20 ms wait) it gives up after 200 us, frees its CU and leaves its
+  // batches to k_finish.
   if (threadIdx.x == 0) {
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     int go = 1;
     while (__hip_atomic_load(&counters[5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
            resolve_blocks) {
-      if (__builtin_amdgcn_s_memrealtime() - t0 > 2000000ull) {
+      if (__builtin_amdgcn_s_memrealtime() - t0 > 20000ull) {   // 200 us of the 100 MHz clock
         go = 0;
         break;
       }
