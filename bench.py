@@ -197,6 +197,9 @@ def main():
     ap.add_argument("--tune", action="append", default=[], metavar="FIELD=VALUE",
                     help="schedule experiment: rc_set_tuning field (repeatable; see "
                          "include/raycast_hip.h rc_tuning); the default is the product schedule")
+    ap.add_argument("--force-group", action="store_true",
+                    help="test aid: take the N>1 code paths (torch.distributed + rc_group over "
+                         "RCCL, sharded step / leg) even with one rank")
     ap.add_argument("--shard", action="store_true",
                     help="N>1 parity: time the row-sharded single image (rc_render_sharded) as "
                          "the step instead of N replicas")
@@ -212,7 +215,12 @@ def main():
     if backend != "nccl":   # rehearsal: ranks share the GPUs, so no RCCL group (replicas only)
         local %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
-    if world > 1:
+    multi = world > 1 or args.force_group
+    if multi:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        os.environ.setdefault("RANK", str(rank))
+        os.environ.setdefault("WORLD_SIZE", str(world))
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
@@ -226,7 +234,7 @@ def main():
     mode = args.mode
     parity = mode == "parity" and args.depth > 0
     group, group_err = None, None
-    if world > 1 and backend == "nccl":
+    if multi and backend == "nccl":
         try:
             group = make_group(pkg, dist, world, rank, local)
         except Exception as e:  # noqa: BLE001 — reported in the line; replicas still run
@@ -288,7 +296,7 @@ def main():
     for _ in range(args.warmup):
         step()
     drain()
-    if world > 1:
+    if multi:
         dist.barrier()
     torch.cuda.synchronize()
     pkg.profile_begin()
@@ -297,7 +305,7 @@ def main():
     for _ in range(args.steps):
         step()
     drain()
-    if world > 1:
+    if multi:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
@@ -306,7 +314,7 @@ def main():
         phases = single_phases
         single["resolve_ms_in_flight"] = round(pipe_tim.get("resolve_ms", 0.0), 4)
     tmax = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-    if world > 1:
+    if multi:
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
     tmax = float(tmax.item())
 
@@ -448,7 +456,7 @@ def main():
         print(json.dumps(line), flush=True)
     if group is not None:
         group.close()
-    if world > 1:
+    if multi:
         dist.destroy_process_group()
 
 

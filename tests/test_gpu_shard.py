@@ -76,6 +76,18 @@ def test_sharded_configs(key, G, scenes, table):
         assert t["dep_pixels"] == table[key].get("dep_pixels", t["dep_pixels"])
 
 
+def test_c5_eight_ranks(scenes, table):
+    """BASELINE C5 as configured — quadric 8192^2 depth 6 over 8 row-sharded ranks (here on
+    one GPU, device copies for the transfers) — md5-equal to the reference in both modes."""
+    g8 = group([0] * 8, "copy")
+    for mode in ("parity", "fast"):
+        key = f"quadric:8192x8192:d6:{mode}"
+        t = {}
+        assert p3_md5(sharded(g8, scenes["quadric"], 8192, 8192, 6, mode, t)) == table[key]["md5"]
+        if mode == "parity":
+            assert t["dep_pixels"] == 11211976   # SURVEY.md §8 a2
+
+
 def test_sharded_ragged_vs_oracle(scenes):
     """Images with fewer rows than ranks, single columns and odd sizes, against the oracle."""
     g5 = group([0] * 5, "copy")
