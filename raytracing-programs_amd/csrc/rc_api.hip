@@ -449,8 +449,13 @@ int ensure_parity(DevCtx& c, FrameBufs& b, int W, int H, rc::ParityWork& w, int 
           hipEventCreateWithFlags(&c.fork, hipEventDisableTiming) != hipSuccess ||
           hipEventCreateWithFlags(&c.join, hipEventDisableTiming) != hipSuccess)
         return -1;
-      c.side_lds = rc::side_lds_bytes(96 * 1024);
+    }
+    // k_side's LDS request must exceed what a resolver workgroup leaves free on its CU, for
+    // the reservation this call's resolver actually makes (the tuning may change it)
+    if (lds > 0 && c.side_for_lds != lds) {
+      c.side_lds = rc::side_lds_bytes(lds);
       c.side_blocks = rc::phase_c_side_blocks(c.cus, c.side_lds);
+      c.side_for_lds = lds;
     }
     if (c.side_blocks > 0 && lds > 0) {   // the guard needs the resolver's LDS reservation
       w.side = c.side;

@@ -97,6 +97,7 @@ struct DevCtx {
   hipStream_t side = nullptr;   // phase C's side stream
   hipEvent_t fork = nullptr, join = nullptr;
   int side_blocks = 0, side_lds = 0;
+  int side_for_lds = -1;        // the resolver LDS reservation side_lds / side_blocks were sized for
   int cus = 256;
   hipStream_t stream = nullptr;
   // event sets: [0] start, then per phase ends (fast: [1] = render; parity: [1] phase A,
