@@ -246,6 +246,8 @@ typedef struct rc_tuning {
   int staged_d2h;         /* 1: pinned bounce buffers + host pool; 0: runtime pageable copy  */
   int prefault;           /* 1: fault the caller's pixmap in while the GPU renders           */
   int copy_threads;       /* host copy pool threads (1..32; fixed at the pool's first use)   */
+  int side_blocks;        /* lone parity frames: at most this many k_side workgroups (phase C
+                             beside the resolver), 0 = one per CU                            */
   int comp_stream;        /* frames in flight: compaction on an unmasked top-priority stream
                              (0 never, 1 always, 2 for images of >= 32 Mpixel)              */
 } rc_tuning;

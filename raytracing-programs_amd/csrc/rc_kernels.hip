@@ -1591,9 +1591,14 @@ __device__ __forceinline__ bool batch_carries(CinG* cin, int ndep, int b, unsign
                                               bool wait, V3& c, bool& hit, TeamState* ts) {
   const int j = b * 64 + (int)(threadIdx.x & 63);
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-  for (;;) {
-    bool ok = true;
-    if (j < ndep) ok = cin_get(cin, j, tag, c, hit);
+  // Only the lanes whose carry-in is still missing poll again (a lane keeps a complete entry),
+  // and the poll interval grows: while the resolver runs, phase C's waiting waves would
+  // otherwise re-read whole batches of agent-scope granules every microsecond and load the
+  // memory fabric the resolver's own hand-offs go through (lone frame: resolver 4.65 ms
+  // beside the waiting side kernel vs 4.48 ms alone).
+  bool ok = j >= ndep;
+  for (int poll = 0;; ++poll) {
+    if (!ok) ok = cin_get(cin, j, tag, c, hit);
     if (__all(ok)) return true;
     if (!wait) return false;
     if (spin_expired(ts, t0)) {
@@ -1602,7 +1607,8 @@ __device__ __forceinline__ bool batch_carries(CinG* cin, int ndep, int b, unsign
       if ((threadIdx.x & 63) == 0) set_error(ts, 2, b * 64 + (__ffsll((long long)miss) - 1), ndep);
       return true;
     }
-    __builtin_amdgcn_s_sleep(32);
+    if (poll < 4) __builtin_amdgcn_s_sleep(32);
+    else __builtin_amdgcn_s_sleep(127);
   }
 }
 
