@@ -1681,6 +1681,15 @@ __device__ __forceinline__ void phase_c_passes(const Scene& sc, const Cam& cam, 
   while (pass1) {
     const int b = wave_ticket(&counters[4]);
     if (b >= nb) break;
+    // one granule first: the batch's last entry (most batches are still unpublished in this
+    // pass; probing all 192 granules of each would put ~1.5 KB of agent-scope loads per batch
+    // on the fabric the resolver's hand-offs use)
+    {
+      const int jl = (b * 64 + 63 < ndep ? b * 64 + 63 : ndep - 1);
+      const unsigned long long g0 =
+          __hip_atomic_load(&cin[jl].g[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (((unsigned)(g0 >> 32) & ~kCinHit) != tag) continue;
+    }
     V3 c = v3(0.0f, 0.0f, 0.0f);
     bool hit = true;
     if (!batch_carries(cin, ndep, b, tag, false, c, hit, ts)) continue;
