@@ -26,7 +26,7 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off \
 CFLAGS   := -O3 -ffp-contract=off -fPIC -Wall -Wno-unused-result -Iinclude -I$(SRC)
 
 HIP_SRCS  := $(SRC)/rc_kernels.hip $(SRC)/rc_api.hip $(SRC)/rc_shard.hip
-HIP_HDRS  := $(SRC)/rc_device.hpp $(SRC)/rc_kernels.h $(SRC)/rc_runtime.h $(SRC)/rc_scene.h include/raycast_hip.h
+HIP_HDRS  := $(SRC)/rc_device.hpp $(SRC)/rc_cudasem.hpp $(SRC)/rc_kernels.h $(SRC)/rc_runtime.h $(SRC)/rc_scene.h include/raycast_hip.h
 FRONT_SRC := $(SRC)/front/parse.c $(SRC)/front/objects.c $(SRC)/front/ppm.c
 
 .PHONY: all oracle ref clean stamps sanitize

@@ -129,7 +129,10 @@ void raycast(json_data_t *json_struct, PPMFormat photo_data);
 /* ---- extended API ------------------------------------------------------------------- */
 
 enum { RC_MODE_PARITY = 0,  /* byte-identical to gcc -O3 C/raycast.c (scan-order carry)   */
-       RC_MODE_FAST   = 1   /* reflection miss ends the bounce loop (CUDA/raycast.cu:224-237) */ };
+       RC_MODE_FAST   = 1,  /* reflection miss ends the bounce loop (CUDA/raycast.cu:224-237) */
+       RC_MODE_CUDA   = 2   /* the CUDA port's semantics: fast's control flow, powf-on-float
+                               arithmetic (CUDA/raycast.cu:455-634, v3math.cu:168), 50 bounces
+                               by default (MAX_ITER, CUDA/raycast.cu:13); parity unpinned */ };
 
 typedef struct rc_options {
   int max_recursion;   /* C/raycast.c:14 MAX_RECURSION; bounce depth = max_recursion - 1 */

@@ -25,7 +25,8 @@ ROOT_DIR = os.path.dirname(PKG_DIR)
 
 MODE_PARITY = 0
 MODE_FAST = 1
-MODES = {"parity": MODE_PARITY, "fast": MODE_FAST}
+MODE_CUDA = 2   # the CUDA port's semantics (include/raycast_hip.h RC_MODE_CUDA)
+MODES = {"parity": MODE_PARITY, "fast": MODE_FAST, "cuda": MODE_CUDA}
 
 
 # ------------------------------------------------------------------ ABI structs --

@@ -308,8 +308,10 @@ void rc_default_options(rc_options* opt, int use_env) {
   if (const char* m = std::getenv("RAYCAST_MODE")) {
     if (!std::strcmp(m, "fast")) opt->mode = RC_MODE_FAST;
     else if (!std::strcmp(m, "parity")) opt->mode = RC_MODE_PARITY;
+    else if (!std::strcmp(m, "cuda")) opt->mode = RC_MODE_CUDA;
     else std::fprintf(stderr, "Warning: unknown RAYCAST_MODE '%s', using parity\n", m);
   }
+  if (opt->mode == RC_MODE_CUDA) opt->max_recursion = 51;   // MAX_ITER 50 bounces
   if (const char* d = std::getenv("RAYCAST_DEPTH")) opt->max_recursion = std::atoi(d) + 1;
   if (const char* g = std::getenv("RAYCAST_GPUS")) opt->num_gpus = std::atoi(g);
   if (const char* v = std::getenv("RAYCAST_DEVICE")) opt->device = std::atoi(v);
@@ -379,8 +381,10 @@ int upload_scene(FrameBufs& b, hipStream_t stream, const rc_scene* s, rc::Launch
   return 0;
 }
 
-// res_cus: CUs the resolver grid may occupy (all of them, or the pipeline's partition).
-int ensure_parity(DevCtx& c, FrameBufs& b, int W, int H, rc::ParityWork& w, int res_cus) {
+// res_cus: CUs the resolver grid may occupy (all of them, or the pipeline's partition);
+// piped: a pipeline lane (< 0: whenever res_cus is not the whole device).
+int ensure_parity(DevCtx& c, FrameBufs& b, int W, int H, rc::ParityWork& w, int res_cus,
+                  int piped_lane) {
   const size_t P = (size_t)W * H;
   if (b.cls.ensure(P) || b.wcarry.ensure(P * sizeof(float4)) ||
       b.deprec.ensure(P * rc::deprec_bytes()) ||
@@ -403,7 +407,7 @@ int ensure_parity(DevCtx& c, FrameBufs& b, int W, int H, rc::ParityWork& w, int 
     if (hipMemset(b.cin.p, 0, b.cin.bytes) != hipSuccess) return -1;
     b.epoch = 1;
   }
-  const bool piped = res_cus != c.cus;
+  const bool piped = piped_lane >= 0 ? piped_lane != 0 : res_cus != c.cus;
   // Resolver placement by its dynamic LDS reservation: one workgroup (4 waves, one per SIMD)
   // per CU for a lone frame, whose critical path is its carry chains (and k_side must stay off
   // the resolver's CUs); two per CU for a pipeline lane, whose grid is small (64 CUs) — there
@@ -537,7 +541,8 @@ int enqueue_render(DevCtx& c, const rc_scene* s, int W, int H, int row0, int row
   if (evset) *evset = ev;
   if (timed) HIP_TRY(hipEventRecord(ev[0], stream));
   if (!parity) {
-    HIP_TRY(rc::launch_render(ls, W, H, row0, row_step, nrows, maxrec, d_out, zc, stream));
+    HIP_TRY(rc::launch_render(ls, W, H, row0, row_step, nrows, maxrec, d_out, zc, stream,
+                              opt->mode == RC_MODE_CUDA));
     if (timed) HIP_TRY(hipEventRecord(ev[1], stream));
     return 0;
   }
@@ -549,7 +554,7 @@ int enqueue_render(DevCtx& c, const rc_scene* s, int W, int H, int row0, int row
   int res_cus = c.cus;   // experiment: single_res_cus sizes the resolver like a pipeline lane's
   if (tune().single_res_cus > 0) res_cus = tune().single_res_cus;
   if (res_cus < 8 || res_cus > c.cus) res_cus = c.cus;
-  if (ensure_parity(c, c.fb, W, H, w, res_cus)) {
+  if (ensure_parity(c, c.fb, W, H, w, res_cus, 0)) {
     std::fprintf(stderr, "Error: out of device memory for the parity workspace\n");
     return -1;
   }
@@ -1149,7 +1154,8 @@ void raycast(json_data_t* json_struct, PPMFormat photo_data) {
                    "\"mode\": \"%s\", \"gpus\": %d}\n",
                    (double)photo_data.width * photo_data.height / (t.total_ms * 1e-3),
                    t.total_ms, t.kernel_ms, t.resolve_ms, t.d2h_ms, (long long)t.dep_pixels,
-                   opt.mode == RC_MODE_FAST ? "fast" : "parity", opt.num_gpus);
+                   opt.mode == RC_MODE_FAST ? "fast" : opt.mode == RC_MODE_CUDA ? "cuda" : "parity",
+                   opt.num_gpus);
   }
   rc_scene_destroy(s);
 }

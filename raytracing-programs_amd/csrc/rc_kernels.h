@@ -76,9 +76,10 @@ constexpr int kCinBytes = 24;         // one carry-in = three tagged 8-byte gran
 constexpr int kLdsShapesMax = 64;
 constexpr int kDenseSlots = 64;       // k_resolve's hand-off ring (helper workgroups at most)     // k_resolve stages up to this many shapes in LDS
 
+// cuda_sem: RC_MODE_CUDA (the CUDA port's arithmetic, rc_cudasem.hpp) instead of fast mode
 hipError_t launch_render(const LaunchScene& s, int W, int H, int row0, int row_step, int nrows,
                          int maxrec, uint8_t* out, unsigned long long* zcount,
-                         hipStream_t stream);
+                         hipStream_t stream, bool cuda_sem = false);
 
 hipError_t launch_parity(const LaunchScene& s, int W, int H, int maxrec, uint8_t* out,
                          const ParityWork& w, unsigned long long* zcount, hipStream_t stream,

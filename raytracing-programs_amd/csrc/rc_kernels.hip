@@ -17,11 +17,14 @@
 //   k_side        side stream, beside the resolver: shade the non-DEP pixels, then every DEP
 //                 pixel with its resolved carry-in (parity phase C) as the carries appear.
 //   k_finish      after the resolver: whatever k_side has not claimed.
+//   k_render_cuda RC_MODE_CUDA: k_render's layout with the CUDA port's arithmetic
+//                 (rc_cudasem.hpp).
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
 #include <cstdlib>
 
+#include "rc_cudasem.hpp"
 #include "rc_device.hpp"
 #include "rc_kernels.h"
 
@@ -207,6 +210,23 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_
   tile_write_rows<kTileW * 3 / 4>(tb.rgb, [&](int q) -> uint8_t* {
     return r0 + q < nrows ? out + ((size_t)(r0 + q) * W + x0) * 3 : nullptr;
   }, nx * 3);
+}
+
+// ------------------------------------------------------- CUDA-port semantics (f4) --
+// One lane per pixel like k_render; up to maxrec - 1 bounces (MAX_ITER, CUDA/raycast.cu:13).
+template <bool kStage>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_PHASE_A_WAVES))) k_render_cuda(
+    Scene sc, Cam cam, int W, int row0, int row_step, int nrows, int maxrec,
+    uint8_t* __restrict__ out) {
+  __shared__ StageBuf<kStage> stage;
+  stage_scene<kStage>(sc, stage);
+  int lx, ly;
+  tile_pixel(lx, ly);
+  const int x = blockIdx.x * kTileW + lx;
+  const int r = blockIdx.y * kTileH + ly;   // local (shard) row
+  if (x >= W || r >= nrows) return;
+  const V3 c = cusem::render_pixel(sc, cam, x, row0 + r * row_step, maxrec - 1);
+  store_rgb(out + ((size_t)r * W + x) * 3, c);
 }
 
 // ------------------------------------------------------------------ parity phase A --
@@ -2085,8 +2105,14 @@ static Cam make_cam(const LaunchScene& s, int W, int H) {
 
 hipError_t launch_render(const LaunchScene& s, int W, int H, int row0, int row_step, int nrows,
                          int maxrec, uint8_t* out, unsigned long long* zcount,
-                         hipStream_t stream) {
+                         hipStream_t stream, bool cuda_sem) {
   dim3 grid((W + kTileW - 1) / kTileW, (nrows + kTileH - 1) / kTileH);
+  if (cuda_sem) {
+    hipLaunchKernelGGL(stage_fits(s) ? k_render_cuda<true> : k_render_cuda<false>, grid,
+                       dim3(kBlock), 0, stream, make_scene(s), make_cam(s, W, H), W, row0,
+                       row_step, nrows, maxrec, out);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(stage_fits(s) ? k_render<true> : k_render<false>, grid, dim3(kBlock), 0, stream, make_scene(s), make_cam(s, W, H),
                      W, H, row0, row_step, nrows, maxrec, out, zcount);
   return hipGetLastError();

@@ -139,7 +139,8 @@ int ctx_get(int device, DevCtx** out);
 int copy_to_host(DevCtx& c, uint8_t* host, const uint8_t* dev, size_t bytes, hipStream_t st);
 void prefault(uint8_t* p, size_t n);
 int upload_scene(FrameBufs& b, hipStream_t stream, const rc_scene* s, rc::LaunchScene& ls);
-int ensure_parity(DevCtx& c, FrameBufs& b, int W, int H, rc::ParityWork& w, int res_cus);
+int ensure_parity(DevCtx& c, FrameBufs& b, int W, int H, rc::ParityWork& w, int res_cus,
+                  int piped_lane = -1);
 int report_spin_error(const FrameBufs& b, const char* where);
 double event_ms(hipEvent_t a, hipEvent_t b);
 // rc_shard.hip: rc_render's multi-GPU path (a cached in-process group over devices

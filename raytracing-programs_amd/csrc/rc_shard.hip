@@ -289,7 +289,7 @@ int render_sharded(rc_group& g, const rc_scene* s, int W, int H, const rc_option
     if (!parity) {
       if (r.nrows > 0)
         HIP_TRY(rc::launch_render(ls[i], W, H, r.rank, G, r.nrows, maxrec, (uint8_t*)r.frame.p,
-                                  zc, r.stream));
+                                  zc, r.stream, opt->mode == RC_MODE_CUDA));
       continue;
     }
     const int lrows = r.nrows > 0 ? r.nrows : 1;

@@ -51,6 +51,8 @@ def oracle_lib():
                                    ctypes.POINTER(RcoStats), ctypes.c_void_p]
         lib.rco_load_scene.argtypes = [ctypes.c_char_p, ctypes.POINTER(rc.JsonDataT)]
         lib.rco_free_scene.argtypes = [ctypes.POINTER(rc.JsonDataT)]
+        lib.rco_render_cuda.argtypes = [ctypes.POINTER(rc.JsonDataT), ctypes.c_int, ctypes.c_int,
+                                        ctypes.c_int, ctypes.c_void_p]
         _oracle = lib
     return _oracle
 
@@ -67,6 +69,24 @@ def oracle_render(scene, width, height, depth=6, mode="parity", with_carry=False
     assert r == 0
     stats = {n: getattr(st, n) for n, _ in RcoStats._fields_}
     return (img, stats, cin) if with_carry else (img, stats)
+
+
+def oracle_render_cuda(scene, width, height, bounces=50):
+    """The CUDA port's semantics restated on the CPU (oracle/rc_oracle_cuda.c)."""
+    img = np.empty((height, width, 3), dtype=np.uint8)
+    r = oracle_lib().rco_render_cuda(ctypes.byref(scene.js), width, height, bounces,
+                                     img.ctypes.data_as(ctypes.c_void_p))
+    assert r == 0
+    return img
+
+
+def read_p3(path):
+    """Decode a P3 file (header "P3 / W H / maxval", then ASCII samples) to [H, W, 3] uint8."""
+    with open(path) as f:
+        tok = f.read().split()
+    assert tok[0] == "P3"
+    w, h = int(tok[1]), int(tok[2])
+    return np.array(tok[4:4 + 3 * w * h], dtype=np.int64).astype(np.uint8).reshape(h, w, 3)
 
 
 def golden_table():

@@ -144,3 +144,16 @@ def test_sharded_repeat_and_stats(scenes, table):
     assert st["ranks"] == 4 and st["dep_pixels"] == 2804464
     assert st["entry_bytes"] == 64 * st["dep_pixels"] and st["carry_bytes"] == 24 * st["dep_pixels"]
     assert st["resolve_ms"] > 0.0 and st["device_ms"] >= st["resolve_ms"]
+
+
+@pytest.mark.parametrize("G", [2, 5])
+def test_sharded_cuda_mode(G, scenes):
+    """RC_MODE_CUDA through the row-sharded path (pixel-parallel like fast mode) against its CPU
+    restatement (oracle/rc_oracle_cuda.c)."""
+    from helpers import oracle_render_cuda
+    g = group([0] * G, "copy")
+    for name in ("reflection", "quadric2"):
+        for d in (6, 50):
+            np.testing.assert_array_equal(sharded(g, scenes[name], 160, 97, d, "cuda"),
+                                          oracle_render_cuda(scenes[name], 160, 97, d),
+                                          err_msg=f"{name} d{d} G{G}")
