@@ -10,7 +10,7 @@ the carry resolvers of consecutive frames run side by side on one CU partition w
 pixel phases run on the other; DESIGN.md §frames in flight) — `value` is K frames' pixels
 over the time to finish all K.  `single_frame` reports one frame at a time
 (rc_render_device, the raycast() path; --inflight 1 makes that the measured step).
-Fast mode: one render kernel per frame.
+Fast mode: one render kernel per frame; cuda mode (the CUDA port's semantics) likewise.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--mode parity|fast] [--inflight 1|2]
 
@@ -182,7 +182,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--mode", default="parity", choices=["parity", "fast"])
+    ap.add_argument("--mode", default="parity", choices=["parity", "fast", "cuda"],
+                    help="cuda: the CUDA port's semantics (RC_MODE_CUDA, SURVEY §8 f4; pass "
+                         "--depth 50 for its MAX_ITER)")
     ap.add_argument("--size", type=int, default=4096)
     ap.add_argument("--depth", type=int, default=6)
     ap.add_argument("--scene", default="quadric")
@@ -247,7 +249,7 @@ def main():
     # the step: fast mode over N GPUs = one image row-sharded (strong); parity over N GPUs =
     # N replicas, one image per GPU (weak: the carry resolver is serial), or the
     # sharded single image with --shard
-    sharded = group is not None and (mode == "fast" or args.shard)
+    sharded = group is not None and (mode in ("fast", "cuda") or args.shard)
     out = torch.empty((H, W, 3), dtype=torch.uint8, device="cuda")
     stream = torch.cuda.current_stream()
 
@@ -357,7 +359,7 @@ def main():
     if rank == 0:
         images = 1 if sharded else world
         value = images * W * H * args.steps / tmax
-        work = WORK.get(f"{args.scene}:{args.size}:{args.depth}")
+        work = WORK.get(f"{args.scene}:{args.size}:{args.depth}") if mode != "cuda" else None
         rows_here = H if not sharded else (H + world - 1) // world
         if parity:
             dom_name, dom_ms = "k_resolve", phases["resolve_ms"]
@@ -451,7 +453,7 @@ def main():
                                    for k, v in shard_stats.items()}
         if world == 1 and not args.timed_only:
             line["end_to_end"] = end_to_end(pkg, scene, W, H, args.depth, mode)
-        if world == 1 and not args.no_cpu_baseline and not args.timed_only:
+        if world == 1 and not args.no_cpu_baseline and not args.timed_only and mode != "cuda":
             line["cpu_baseline"] = cpu_baseline(scene_path, args.size, args.depth)
         print(json.dumps(line), flush=True)
     if group is not None:
