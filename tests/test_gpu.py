@@ -429,3 +429,21 @@ def test_cuda_mode_cli_and_device(tmp_path, scenes):
     rc.render_device(scenes["reflection"], 200, 150, d.data_ptr(), depth=50, mode="cuda")
     torch.cuda.synchronize()
     np.testing.assert_array_equal(d.cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("a0", [-2, -5, 2.5, 7.25])
+def test_spot_exponents_beyond_references(a0, tmp_path):
+    """Spot exponents no reference scene has (negative integers: pown_dd's reciprocal;
+    non-integers: the device pow) against the oracle's glibc pow, both modes — image-level
+    parity (scripts/spot_exp_probe.py covers more cases)."""
+    base = open(scene_path("reflection")).read().rstrip("\n")
+    path = tmp_path / "spot.scene"
+    path.write_text(base + "\nlight, color: [1.5, 1.2, 1.0], radial-a2: 0.01, radial-a1: 0.0125, "
+                    "radial-a0: 0.0125, position: [0, 2, 0], theta: 0.9, "
+                    f"angular-a0: {a0}, direction: [0, -0.3, -1]\n")
+    s = rc.Scene.from_file(str(path))
+    for mode in ("fast", "parity"):
+        want, st = oracle_render(s, 128, 128, 4, mode)
+        assert st["parity_defined"]
+        np.testing.assert_array_equal(rc.render(s, 128, 128, depth=4, mode=mode), want,
+                                      err_msg=f"a0={a0} {mode}")
