@@ -405,14 +405,122 @@ __device__ __forceinline__ int nearest_primary(const Scene& sc, V3 D, float& tbe
   return idx;
 }
 
+// ------------------------------------------------------------------- shadow rays --
+// A shadow ray only asks whether some shape is hit with 0 < t < inf (C/raycast.c:441-531
+// with shadow_test = true); t itself is never used.  t = (float)(num / den) with an IEEE
+// double quotient, so its class follows from the operands' signs and exponents alone when
+// both are normal doubles whose biased exponents differ by e in [-148, 126]: then
+// |num/den| lies in (2^(e-1), 2^(e+1)), which RN64 and then RN32 (both monotone, both
+// bounds representable) keep inside [2^-149, 2^127] — a non-zero finite float of the
+// quotient's sign.  Anything else (a zero, subnormal, inf or NaN operand, or an extreme
+// ratio) takes the division as written.  Saves one or two f64 divisions per shadow test.
+constexpr int kQNeg = 0, kQZero = 1, kQPos = 2, kQOther = 3;   // t < 0, t = +-0, 0<t<inf, inf/NaN
+__device__ __forceinline__ int quot_class(double num, double den) {
+  const unsigned hn = (unsigned)__double2hiint(num), hd = (unsigned)__double2hiint(den);
+  const int en = (int)((hn >> 20) & 0x7ffu), ed = (int)((hd >> 20) & 0x7ffu);
+  const int e = en - ed;
+  if (en != 0 && en != 0x7ff && ed != 0 && ed != 0x7ff && e >= -148 && e <= 126)
+    return ((hn ^ hd) >> 31) ? kQNeg : kQPos;
+  const float t = (float)(num / den);
+  if (t < 0.0f) return kQNeg;
+  if (t == 0.0f) return kQZero;
+  return t < __builtin_inff() ? kQPos : kQOther;
+}
+
+// hit_sphere as a shadow test: the first root unless it is negative (C/raycast.c:593-597)
+__device__ __forceinline__ bool shadow_sphere(V3 O, V3 D, const rc_shape& s, RayK k) {
+  V3 tv = v3(O.x - s.p[0], O.y - s.p[1], O.z - s.p[2]);
+  float b = 2.0f * dot(D, tv);
+  float c = (float)((double)dot(tv, tv) - s.r2);
+  float fac = k.a4 * c;
+  float disc = (float)((double)b * (double)b - (double)fac);
+  if (disc < 0.0f) return false;
+  double sq = sqrt_ns((double)disc);
+  int q = quot_class((double)(-b) - sq, k.den);
+  if (q == kQNeg) q = quot_class((double)(-b) + sq, k.den);
+  return q == kQPos;
+}
+
+// hit_quadric + the bounce rays' z rule as a shadow test.  The z rule (C/raycast.c:492-494)
+// needs t itself when it can fire, i.e. for a positive t only if D.z < 0: then the chosen
+// root's quotient is formed exactly as in hit_quadric.
+__device__ __forceinline__ bool shadow_quadric(V3 O, V3 D, const rc_shape& q, int skip) {
+  double acc;
+  acc = q.A * ((double)D.x * (double)D.x);
+  acc = acc + q.B * ((double)D.y * (double)D.y);
+  acc = acc + q.C * ((double)D.z * (double)D.z);
+  acc = acc + (double)(q.qd * D.x * D.y);
+  acc = acc + (double)(q.qe * D.x * D.z);
+  acc = acc + (double)(q.qf * D.y * D.z);
+  const float aq = (float)acc;
+
+  acc = 2.0 * q.A * (double)O.x * (double)D.x;
+  acc = acc + 2.0 * q.B * (double)O.y * (double)D.y;
+  acc = acc + 2.0 * q.C * (double)O.z * (double)D.z;
+  acc = acc + (double)(q.qd * (O.x * D.y + O.y * D.x));
+  acc = acc + (double)(q.qe * (O.x * D.z + O.z * D.x));
+  acc = acc + (double)(q.qf * (O.y * D.z + O.z * D.y));
+  acc = acc + (double)(q.qg * D.x);
+  acc = acc + (double)(q.qh * D.y);
+  acc = acc + (double)(q.qi * D.z);
+  const float bq = (float)acc;
+
+  acc = q.A * ((double)O.x * (double)O.x);
+  acc = acc + q.B * ((double)O.y * (double)O.y);
+  acc = acc + q.C * ((double)O.z * (double)O.z);
+  acc = acc + (double)(q.qd * O.x * O.y);
+  acc = acc + (double)(q.qe * O.x * O.z);
+  acc = acc + (double)(q.qf * O.y * O.z);
+  acc = acc + (double)(q.qg * O.x);
+  acc = acc + (double)(q.qh * O.y);
+  acc = acc + (double)(q.qi * O.z);
+  acc = acc + (double)q.qj;
+  const float cq = (float)acc;
+
+  double num, den;
+  int cls;
+  if ((double)aq == 0.0) {
+    num = -1.0 * (double)cq;
+    den = (double)bq;
+    cls = quot_class(num, den);
+  } else {
+    const float disc = (float)((double)bq * (double)bq - 4.0 * (double)aq * (double)cq);
+    if ((double)disc < 0.0) return false;
+    den = 2.0 * (double)aq;
+    const double sq = sqrt_ns((double)disc);
+    num = (double)(-bq) - sq;
+    cls = quot_class(num, den);
+    if (cls == kQNeg || cls == kQZero) {
+      num = (double)(-bq) + sq;
+      cls = quot_class(num, den);
+    }
+  }
+  if (cls != kQPos) return false;
+  if (skip != -1 && D.z < 0.0f) {
+    const float t = (float)(num / den);
+    if ((O.z + t * D.z) < O.z) return false;
+  }
+  return true;
+}
+
 // C/raycast.c:441-531 (shadow_test = true): is any shape hit with 0 < t < inf?  The first
 // such shape is always accepted, so the loop may stop there.
 __device__ __forceinline__ bool shadowed(const Scene& sc, V3 O, V3 D, int skip) {
   const RayK rk = ray_consts(D);
   for (int k = 0; k < sc.n; ++k) {
-    float t = 0.0f;
-    const bool hit = test_shape(sc.shapes[k], O, D, rk, skip, t);
-    if (hit && k != skip && __builtin_inff() > t && t > 0.0f) return true;
+    if (k == skip) continue;
+    const rc_shape& s = sc.shapes[k];
+    const int type = s.type;
+    bool hit = false;
+    if (type == RC_SHAPE_SPHERE) {
+      hit = shadow_sphere(O, D, s, rk);
+    } else if (type == RC_SHAPE_PLANE) {
+      float t = 0.0f;
+      hit = hit_plane(O, D, s, t) && __builtin_inff() > t && t > 0.0f;
+    } else if (type == RC_SHAPE_QUADRIC) {
+      hit = shadow_quadric(O, D, s, skip);
+    }
+    if (hit) return true;
   }
   return false;
 }
