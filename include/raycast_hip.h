@@ -230,7 +230,7 @@ typedef struct rc_tuning {
   int resolve_lds_kb;     /* resolver LDS reservation in KiB, 0 = by path (96 / 56)        */
   int resolve_grid;       /* resolver workgroups, 0 = resident capacity (>= 8 otherwise)   */
   int team_blocks;        /* long-segment team workgroups, -1 = by path (128 / 3/8 grid)   */
-  int helpers;            /* dense-run helper workgroups (0..64)                            */
+  int helpers;            /* dense-run helper workgroups of a lone frame (0..64; pipeline lanes use none) */
   int hand_run;           /* changes in a row before a wave hands its run to a helper       */
   int long_len;           /* segments of >= long_len entries go to the team                 */
   int wave_k;             /* clean cooperative steps before a wave window returns to LANE   */

@@ -494,8 +494,12 @@ int ensure_parity(DevCtx& c, FrameBufs& b, int W, int H, rc::ParityWork& w, int 
   if (tu.team_blocks >= 0) w.team_blocks = tu.team_blocks;
   if (w.team_blocks > 256) w.team_blocks = 256;
   if (w.team_blocks > w.resolve_blocks / 2) w.team_blocks = w.resolve_blocks / 2;
-  // helper blocks for handed-off dense runs (k_resolve): 8 of the grid
-  w.helpers = tu.helpers;
+  // helper blocks for handed-off dense runs (k_resolve): 8 of the grid for a lone frame
+  // (quadric 4096^2 5.85 -> 5.64 ms); none in a pipeline lane, whose grid is a partition's and
+  // whose regular waves need those slots more (frames in flight without helpers: reflection
+  // 2048^2 d4 7.5e9 -> 8.0e9 rays/s, quadric 8192^2 8.3e9 -> 8.8e9, quadric 4096^2 +1 %,
+  // scripts/helper_sweep.sh)
+  w.helpers = piped ? 0 : tu.helpers;
   if (w.helpers < 0) w.helpers = 0;
   if (w.helpers > rc::kDenseSlots) w.helpers = rc::kDenseSlots;   // one ring slot per helper
   if (w.team_blocks + w.helpers > w.resolve_blocks * 3 / 4) w.helpers = 0;

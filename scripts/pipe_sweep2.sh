@@ -10,3 +10,8 @@ run --tune pipe_res_cus=160
 run --tune pipe_resolvers=3 --tune pipe_res_cus=160 --tune pipe_slots=5
 run --tune pipe_resolvers=3 --tune pipe_res_cus=192 --tune pipe_slots=5
 run
+# simple 1024^2 d6 (slower resolver than round 1's v10 line: 0.54 vs 0.41 ms)
+run --scene simple --size 1024
+run --scene simple --size 1024 --tune helpers=0
+run --scene simple --size 1024 --tune team_blocks=0
+run --scene simple --size 1024 --tune helpers=0 --tune team_blocks=0
