@@ -224,7 +224,8 @@ int rc_profile_end(rc_phase_stats *out);
  * top of it.  Takes effect at the next render (the frame pipeline's layout at its next
  * build: rc_pipe_reset). */
 typedef struct rc_tuning {
-  int side;               /* 1: a lone parity frame's phase C runs beside the resolver     */
+  int side;               /* a lone parity frame's phase C beside the resolver: 0 never,  
+                             1 always, 2 for images of >= 8 Mpixel (default)              */
   int split_shade;        /* 1: phase A's colours move beside the resolver (needs side)    */
   int resolve_shared;     /* 1: no one-resolver-workgroup-per-CU LDS reservation           */
   int resolve_lds_kb;     /* resolver LDS reservation in KiB, 0 = by path (96 / 56)        */

@@ -35,7 +35,7 @@ std::mutex g_ctx_mu;
 
 rc_tuning default_tuning() {
   rc_tuning t;
-  t.side = 1;
+  t.side = 2;
   t.split_shade = 0;
   t.resolve_shared = 0;
   t.resolve_lds_kb = 0;
@@ -278,7 +278,7 @@ int rc_set_tuning(const rc_tuning* t) {
   if (!t) return -1;
   auto in = [](int v, int lo, int hi) { return v >= lo && v <= hi; };
   const bool ok =
-      in(t->side, 0, 1) && in(t->split_shade, 0, 1) && in(t->resolve_shared, 0, 1) &&
+      in(t->side, 0, 2) && in(t->split_shade, 0, 1) && in(t->resolve_shared, 0, 1) &&
       in(t->resolve_lds_kb, 0, 152) && (t->resolve_grid == 0 || in(t->resolve_grid, 8, 1 << 16)) &&
       in(t->team_blocks, -1, 256) && in(t->helpers, 0, rc::kDenseSlots) &&
       in(t->hand_run, 1, 1 << 30) && in(t->long_len, 64, 1 << 30) && in(t->wave_k, 1, 64) &&
@@ -448,7 +448,12 @@ int ensure_parity(DevCtx& c, FrameBufs& b, int W, int H, rc::ParityWork& w, int 
   w.rready = w.rdone = w.rt0 = w.rt1 = nullptr;
   w.split_shade = tu.split_shade ? 1 : 0;
   if (piped) w.split_shade = 0;   // phase C after the resolver, on the pixel partition
-  if (!piped && tu.side) {   // phase C overlapped with the resolver
+  // phase C beside the resolver: always (side 1), or (side 2, the default) for images of
+  // >= 8 Mpixel — below that phase C after the resolver is short and the side kernel's
+  // census / k_finish tail costs more (lone simple 1024^2 d6 0.746 -> 0.680 ms, reflection
+  // 2048^2 d4 1.045 -> 1.003 ms without it; quadric 4096^2 +0.5 ms, 8192^2 +2.2 ms)
+  const bool side = tu.side == 1 || (tu.side == 2 && P >= ((size_t)8 << 20));
+  if (!piped && side) {   // phase C overlapped with the resolver
     if (!c.side) {
       if (hipStreamCreateWithFlags(&c.side, hipStreamNonBlocking) != hipSuccess ||
           hipEventCreateWithFlags(&c.fork, hipEventDisableTiming) != hipSuccess ||
@@ -475,6 +480,7 @@ int ensure_parity(DevCtx& c, FrameBufs& b, int W, int H, rc::ParityWork& w, int 
       w.side_lds = c.side_lds;
     }
   }
+  if (!w.side) w.split_shade = 0;   // split shading needs the side kernel
   w.epoch = b.epoch;
   w.counters = (int*)b.counters.p;
   w.team = b.team.p;

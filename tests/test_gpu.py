@@ -57,7 +57,8 @@ def test_configs(key, scenes, table):
     assert p3_md5(img) == table[key]["md5"], key
 
 
-SCHEDULES = {"no-side": dict(side=0), "split-shade": dict(split_shade=1),
+SCHEDULES = {"no-side": dict(side=0), "side-always": dict(side=1),
+             "split-shade": dict(split_shade=1, side=1),
              "resolve-shared": dict(resolve_shared=1), "no-dep-fast": dict(dep_fast=0),
              "no-side+no-dep-fast": dict(side=0, dep_fast=0),
              "no-side+phase-c-finish": dict(side=0, phase_c_finish=1), "no-o0": dict(o0=0),
@@ -71,7 +72,8 @@ SCHEDULES = {"no-side": dict(side=0), "split-shade": dict(split_shade=1),
 def test_parity_schedules(sched, scenes, table):
     """The parity pipeline's alternative schedules (rc_set_tuning) give the same bytes:
     phase C after the resolver only (side=0: clean entries, then full waves of the rest —
-    k_dep_chunks; with phase_c_finish through k_finish's batch claims), colours shaded beside
+    k_dep_chunks; with phase_c_finish through k_finish's batch claims), phase C beside the
+    resolver at every size (side=1; by default only from 8 Mpixel), colours shaded beside
     the resolver (split_shade), no one-workgroup-per-CU reservation (resolve_shared, which
     also disables the side stream), every first-bounce-miss pixel recomputed in phase C
     (dep_fast=0), primary rays through the general intersection tests instead of the origin-
