@@ -35,6 +35,7 @@ import json
 import os
 import subprocess
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -336,26 +337,6 @@ def main():
         pkg.render_device(scene, W, H, out.data_ptr(), stream.cuda_stream, depth=args.depth,
                           mode=mode, timing=tim)
     torch.cuda.synchronize()
-    # N>1 parity replicas: the sharded single image as well, reported beside (never as) value
-    shard_leg = None
-    if group is not None and not sharded and not args.timed_only:
-        dist.barrier()
-        group.render(scene, W, H, out.data_ptr(), depth=args.depth, mode=mode)   # warm
-        dist.barrier()
-        ts = time.perf_counter()
-        reps = 5
-        for _ in range(reps):
-            group.render(scene, W, H, out.data_ptr(), depth=args.depth, mode=mode)
-        dist.barrier()
-        ms = (time.perf_counter() - ts) * 1e3 / reps
-        st = group.stats()
-        shard_leg = {"value": round(W * H / (ms * 1e-3), 1), "unit": "rays/s", "ms": round(ms, 4),
-                     "note": f"one {W}x{H} image row-sharded over {world} GPUs (rc_render_sharded: "
-                             "phase A on every rank, DEP entries gathered to rank 0 over RCCL, "
-                             "serial carry resolver there, carry-ins back, phase C on every rank, "
-                             "row blocks gathered); strong scaling, capped by the resolver",
-                     "stats": {k: (round(v, 4) if isinstance(v, float) else v)
-                               for k, v in (st or {}).items()}}
     if rank == 0:
         images = 1 if sharded else world
         value = images * W * H * args.steps / tmax
@@ -444,8 +425,6 @@ def main():
         }
         if single:
             line["single_frame"] = single
-        if shard_leg:
-            line["sharded_single_image"] = shard_leg
         if group_err:
             line["group_error"] = group_err
         if sharded:
@@ -455,6 +434,45 @@ def main():
             line["end_to_end"] = end_to_end(pkg, scene, W, H, args.depth, mode)
         if world == 1 and not args.no_cpu_baseline and not args.timed_only and mode != "cuda":
             line["cpu_baseline"] = cpu_baseline(scene_path, args.size, args.depth)
+    # N>1 parity replicas: the sharded single image as well, reported beside (never as) value.
+    # It is the only multi-process RCCL exchange of the run, so a watchdog bounds it: if it has
+    # not finished in LEG_TIMEOUT_S, rank 0 prints the line with the leg marked as timed out
+    # and every rank exits (the timed region's result is never lost to a stuck exchange).
+    LEG_TIMEOUT_S = 120
+    leg_done = threading.Event()
+
+    def leg_watchdog():
+        if leg_done.wait(LEG_TIMEOUT_S):
+            return
+        if rank == 0:
+            line["sharded_single_image"] = {"error": f"timed out after {LEG_TIMEOUT_S} s"}
+            print(json.dumps(line), flush=True)
+        os._exit(0)
+
+    shard_leg = None
+    if group is not None and not sharded and not args.timed_only:
+        threading.Thread(target=leg_watchdog, daemon=True).start()
+        dist.barrier()
+        group.render(scene, W, H, out.data_ptr(), depth=args.depth, mode=mode)   # warm
+        dist.barrier()
+        ts = time.perf_counter()
+        reps = 5
+        for _ in range(reps):
+            group.render(scene, W, H, out.data_ptr(), depth=args.depth, mode=mode)
+        dist.barrier()
+        ms = (time.perf_counter() - ts) * 1e3 / reps
+        st = group.stats()
+        shard_leg = {"value": round(W * H / (ms * 1e-3), 1), "unit": "rays/s", "ms": round(ms, 4),
+                     "note": f"one {W}x{H} image row-sharded over {world} GPUs (rc_render_sharded: "
+                             "phase A on every rank, DEP entries gathered to rank 0 over RCCL, "
+                             "serial carry resolver there, carry-ins back, phase C on every rank, "
+                             "row blocks gathered); strong scaling, capped by the resolver",
+                     "stats": {k: (round(v, 4) if isinstance(v, float) else v)
+                               for k, v in (st or {}).items()}}
+    leg_done.set()
+    if rank == 0:
+        if shard_leg:
+            line["sharded_single_image"] = shard_leg
         print(json.dumps(line), flush=True)
     if group is not None:
         group.close()
