@@ -1610,18 +1610,28 @@ __device__ __forceinline__ bool batch_claim(int* state, int b) {
 __device__ __forceinline__ bool batch_carries(CinG* cin, int ndep, int b, unsigned tag,
                                               bool wait, V3& c, bool& hit, TeamState* ts) {
   const int j = b * 64 + (int)(threadIdx.x & 63);
-  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   // Only the lanes whose carry-in is still missing poll again (a lane keeps a complete entry),
   // and the poll interval grows: while the resolver runs, phase C's waiting waves would
   // otherwise re-read whole batches of agent-scope granules every microsecond and load the
   // memory fabric the resolver's own hand-offs go through (lone frame: resolver 4.65 ms
   // beside the waiting side kernel vs 4.48 ms alone).
+  // The limit measures a lack of progress: it restarts whenever another of the
+  // batch's carry-ins arrives or another regular resolver wave finishes, so a legitimately
+  // long resolver (huge frames, scenes whose shapes are not staged in LDS) is not cut off.
   bool ok = j >= ndep;
+  unsigned long long t0 = 0;
+  int seen = -1;
   for (int poll = 0;; ++poll) {
     if (!ok) ok = cin_get(cin, j, tag, c, hit);
     if (__all(ok)) return true;
     if (!wait) return false;
-    if (spin_expired(ts, t0)) {
+    const int progress =
+        __popcll(__ballot(ok)) +
+        __hip_atomic_load(&ts->dq.finished, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (progress != seen) {
+      seen = progress;
+      t0 = __builtin_amdgcn_s_memrealtime();
+    } else if (spin_expired(ts, t0)) {
       // the first entry of the batch that is still missing
       const unsigned long long miss = __ballot(!ok);
       if ((threadIdx.x & 63) == 0) set_error(ts, 2, b * 64 + (__ffsll((long long)miss) - 1), ndep);
