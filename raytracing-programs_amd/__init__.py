@@ -15,6 +15,7 @@ name has a hyphen; ``__graft_entry__`` and tests load it by path).
 import ctypes
 import os
 import sys
+import threading
 
 import numpy as np
 
@@ -147,8 +148,19 @@ def _one_hip_runtime():
         pass
 
 
+_HIP_LOCK = threading.Lock()
+
+
 def hip_lib():
-    # RC_HIP_LIB selects a diagnostic build (e.g. libraycast_hip_stamps.so); never the default
+    # RC_HIP_LIB selects a diagnostic build (e.g. libraycast_hip_stamps.so); never the default.
+    # Under a lock: threads making their first call at once must not load the library while
+    # another is still importing torch (a half-imported torch is already in sys.modules, and
+    # the library would then map /opt/rocm's HIP runtime beside torch's: _one_hip_runtime).
+    with _HIP_LOCK:
+        return _hip_lib_locked()
+
+
+def _hip_lib_locked():
     _one_hip_runtime()
     lib = _load(os.environ.get("RC_HIP_LIB", "libraycast_hip.so"))
     lib.rc_scene_create.argtypes = [ctypes.POINTER(JsonDataT)]
@@ -192,6 +204,9 @@ _libc = ctypes.CDLL(None)
 _libc.fopen.restype = ctypes.c_void_p
 _libc.fopen.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
 _libc.fclose.argtypes = [ctypes.c_void_p]
+
+
+_PACK_LOCK = threading.Lock()
 
 
 class Scene:
@@ -240,12 +255,13 @@ class Scene:
 
     def packed(self):
         """rc_scene handle (packed image + phantom record) for the HIP library."""
-        if self._packed is None:
-            h = hip_lib().rc_scene_create(ctypes.byref(self.js))
-            if not h:
-                raise RuntimeError("rc_scene_create failed")
-            self._packed = h
-        return self._packed
+        with _PACK_LOCK:   # render threads sharing a Scene create its handle once
+            if self._packed is None:
+                h = hip_lib().rc_scene_create(ctypes.byref(self.js))
+                if not h:
+                    raise RuntimeError("rc_scene_create failed")
+                self._packed = h
+            return self._packed
 
     def parity_defined(self):
         return bool(hip_lib().rc_scene_parity_defined(self.packed()))

@@ -1043,6 +1043,10 @@ int rc_render(const rc_scene* s, int W, int H, const rc_options* opt, uint8_t* p
   const bool parity = opt->mode == RC_MODE_PARITY && opt->max_recursion > 1;
   const size_t row_bytes = (size_t)W * 3;
   if (G > 1) {   // row shards over RCCL (rc_shard.hip), the image on the first device
+    // one sharded call at a time: d_image is the cached group's root buffer, which the next
+    // caller's render would overwrite before this caller's copy-out
+    static std::mutex group_call_mu;
+    std::lock_guard<std::mutex> one_group_call(group_call_mu);
     uint8_t* d_image = nullptr;
     rc_timing tg;
     if (render_local_group(opt->device, G, s, W, H, opt, &d_image, &tg)) return -1;
@@ -1066,9 +1070,11 @@ int rc_render(const rc_scene* s, int W, int H, const rc_options* opt, uint8_t* p
   const int dev = opt->device;
   DevCtx* c;
   if (hipSetDevice(dev) != hipSuccess || ctx_get(dev, &c)) return -1;
+  // the lock covers the workspace from its (re)allocation on: a concurrent caller's ensure()
+  // could otherwise free the buffer another caller is rendering into
+  std::lock_guard<std::mutex> lk(c->mu);
   if (c->out.ensure((size_t)H * row_bytes)) return -1;
   uint8_t* d_out = (uint8_t*)c->out.p;
-  std::lock_guard<std::mutex> lk(c->mu);
   // parity: the copy overlaps the resolver (copy_overlapped); split shading leaves the non-DEP
   // colours to phase C, so its framebuffer is not final after phase A
   const bool overlap = parity && !tune().split_shade && tune().overlap_d2h;

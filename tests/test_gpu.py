@@ -449,3 +449,33 @@ def test_spot_exponents_beyond_references(a0, tmp_path):
         assert st["parity_defined"]
         np.testing.assert_array_equal(rc.render(s, 128, 128, depth=4, mode=mode), want,
                                       err_msg=f"a0={a0} {mode}")
+
+
+def test_concurrent_callers_one_device(scenes, table):
+    """Host threads calling raycast()/rc_render on the same device at once (ctypes drops the
+    GIL): the per-device lock serialises them on the shared workspace, the resolver's
+    TeamState and the copy pool, so every image stays byte-identical."""
+    import threading
+    keys = ["quadric:1024x1024:d6:parity", "reflection:2048x2048:d4:parity",
+            "simple:1024x1024:d6:fast", "quadric:512x384:d6:parity"] * 2
+    got, errs = {}, []
+
+    def worker(i, key):
+        try:
+            scene, size, d, mode = key.split(":")
+            w, h = map(int, size.split("x"))
+            for rep in range(3):
+                img = rc.render(scenes[scene], w, h, depth=int(d[1:]), mode=mode)
+                got[(i, rep)] = (key, p3_md5(img))
+        except Exception as e:   # pragma: no cover - reported below
+            errs.append(repr(e))
+
+    ts = [threading.Thread(target=worker, args=(i, k)) for i, k in enumerate(keys)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(100)
+    assert not errs, errs
+    assert len(got) == 3 * len(keys)
+    for (key, md5) in got.values():
+        assert md5 == table[key]["md5"], key
