@@ -71,7 +71,7 @@ def load_pkg():
 
 # rocprofv3 --pmc summaries of this exact configuration from HEAD (scripts/pmc_valu.sh,
 # scripts/pmc_fast.sh -> scripts/pmc_summary.py): per-kernel counter means per launch.
-PMC_PROFILES = {("quadric", 4096, 6, "parity"): "profiles/r02c_pmc_lone_4096.json",
+PMC_PROFILES = {("quadric", 4096, 6, "parity"): "profiles/r02g_pmc_lone_4096.json",
                 ("quadric", 4096, 6, "fast"): "profiles/r02c_pmc_fast_4096.json"}
 
 
