@@ -12,6 +12,7 @@ import ctypes
 import os
 import re
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -228,3 +229,21 @@ def test_tuning_api_validates():
     assert rc.get_tuning() == base
     with pytest.raises(KeyError):
         rc.set_tuning(no_such_field=1)
+
+
+def test_binding_loads_one_hip_runtime_from_threads():
+    """Threads making their first binding call at once load libraycast_hip.so once, after
+    torch: exactly one HIP runtime is mapped (a second one, from /opt/rocm beside torch's,
+    corrupts the heap at exit; seen when 8 render threads raced torch's import)."""
+    code = (
+        "import sys, threading\n"
+        "import importlib.util as u\n"
+        f"spec = u.spec_from_file_location('rc', {os.path.join(ROOT, 'raytracing-programs_amd', '__init__.py')!r})\n"
+        "rc = u.module_from_spec(spec); spec.loader.exec_module(rc)\n"
+        "ts = [threading.Thread(target=rc.hip_lib) for _ in range(8)]\n"
+        "[t.start() for t in ts]; [t.join() for t in ts]\n"
+        "maps = {l.split()[-1] for l in open('/proc/self/maps') if 'libamdhip64' in l}\n"
+        "print(len(maps), sorted(maps))\n")
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert out.stdout.split()[0] == "1", out.stdout
