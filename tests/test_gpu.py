@@ -479,3 +479,46 @@ def test_concurrent_callers_one_device(scenes, table):
     assert len(got) == 3 * len(keys)
     for (key, md5) in got.values():
         assert md5 == table[key]["md5"], key
+
+
+def test_lone_renders_beside_frames_in_flight(scenes, table):
+    """A caller's raycast()/rc_render issued while another thread's frames are still in
+    flight (rc_frame_submit without rc_frames_wait): the lone frame's resolver waits for CUs
+    the pipeline's resolvers hold (its team spins are bounded, the pipeline's resolvers never
+    wait on it), and every image of both callers is byte-identical."""
+    import threading
+    torch = pytest.importorskip("torch")
+    seq = ["quadric:4096x4096:d6:parity", "reflection:2048x2048:d4:parity"] * 4
+    bufs = []
+    for key in seq:
+        _, size, _, _ = key.split(":")
+        w, h = map(int, size.split("x"))
+        bufs.append(torch.zeros((h, w, 3), dtype=torch.uint8, device="cuda"))
+    torch.cuda.synchronize()
+    lone, errs = [], []
+
+    def lone_caller():
+        try:
+            for key in ["quadric:4096x4096:d6:parity", "quadric:512x384:d6:parity"] * 2:
+                scene, size, d, mode = key.split(":")
+                w, h = map(int, size.split("x"))
+                img = rc.render(scenes[scene], w, h, depth=int(d[1:]), mode=mode)
+                lone.append((key, p3_md5(img)))
+        except Exception as e:   # pragma: no cover - reported below
+            errs.append(repr(e))
+
+    t = threading.Thread(target=lone_caller)
+    for i, (key, buf) in enumerate(zip(seq, bufs)):
+        scene, size, d, mode = key.split(":")
+        w, h = map(int, size.split("x"))
+        rc.frame_submit(scenes[scene], w, h, buf.data_ptr(), depth=int(d[1:]), mode=mode)
+        if i == 1:
+            t.start()
+    t.join(100)
+    rc.frames_wait({})
+    assert not errs, errs
+    assert len(lone) == 4
+    for key, md5 in lone:
+        assert md5 == table[key]["md5"], ("lone", key)
+    for key, buf in zip(seq, bufs):
+        assert p3_md5(buf.cpu().numpy()) == table[key]["md5"], ("in flight", key)
