@@ -57,6 +57,8 @@ WORK = {
 }
 PEAK_FP64_TFLOPS = 78.6    # MI355X vector FP64 (MI355X_MICROARCH.md: FP32 157.3 / 2)
 PEAK_HBM_GBS = 8000.0      # MI355X HBM3E
+GOLDEN_MD5 = os.path.join(ROOT, "tests", "golden", "md5.json")   # the reference's own outputs
+LEG_TIMEOUT_EXIT = 3       # exit status when the sharded leg's watchdog fires
 
 
 def load_pkg():
@@ -120,6 +122,51 @@ def end_to_end(pkg, scene, W, H, depth, mode, reps=5):
                     "rc_render's own clock"}
 
 
+def golden_md5(scene, W, H, depth, mode):
+    """md5 of the reference's P3 output for this configuration (tests/golden/md5.json, made by
+    the reference build itself), or None when the table has no such image."""
+    try:
+        with open(GOLDEN_MD5) as f:
+            e = json.load(f).get(f"{scene}:{W}x{H}:d{depth}:{mode}")
+    except OSError:
+        return None
+    return e["md5"] if e else None
+
+
+def verify_frames(pkg, bufs, want_md5):
+    """Outside the timed region: every timed frame's bytes against frame 0's (torch.equal on
+    the device) and frame 0's P3 md5 against the reference's golden.  Returns (frames whose
+    bytes equal frame 0's, frame 0's md5, golden match or None without a golden)."""
+    import torch
+    ref = bufs[0]
+    equal = sum(1 for b in bufs if torch.equal(b, ref))
+    md5 = pkg.p3_md5(ref.cpu().numpy())
+    return equal, md5, (None if want_md5 is None else md5 == want_md5)
+
+
+def run_leg_with_watchdog(leg, timeout_s, on_timeout):
+    """Run leg() under a watchdog: if it has not returned after timeout_s (a stuck
+    multi-process exchange), on_timeout() runs (rank 0 prints the line with the leg marked as
+    timed out, so the timed result is not lost) and the process exits with LEG_TIMEOUT_EXIT —
+    never 0, so the driver sees the hang."""
+    done = threading.Event()
+
+    def watch():
+        if done.wait(timeout_s):
+            return
+        try:
+            on_timeout()
+        finally:
+            sys.stdout.flush()
+            os._exit(LEG_TIMEOUT_EXIT)
+
+    threading.Thread(target=watch, daemon=True).start()
+    try:
+        return leg()
+    finally:
+        done.set()
+
+
 def cpu_model():
     try:
         with open("/proc/cpuinfo") as f:
@@ -131,37 +178,114 @@ def cpu_model():
     return None
 
 
+def _cpu_jiffies():
+    """{cpu: (busy, total)} from /proc/stat."""
+    out = {}
+    with open("/proc/stat") as f:
+        for line in f:
+            if line.startswith("cpu") and line[3:4].isdigit():
+                name, *v = line.split()
+                v = [int(x) for x in v]
+                idle = v[3] + (v[4] if len(v) > 4 else 0)
+                out[int(name[3:])] = (sum(v) - idle, sum(v))
+    return out
+
+
+def _siblings(c):
+    """The hardware threads sharing core c (SMT siblings), c included."""
+    try:
+        with open(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list") as f:
+            out = set()
+            for part in f.read().strip().split(","):
+                lo, _, hi = part.partition("-")
+                out.update(range(int(lo), int(hi or lo) + 1))
+            return out
+    except (OSError, ValueError):
+        return {c}
+
+
+def quiet_core(cands, window_s=0.5):
+    """The least busy core of `cands` over a short window, judged with its SMT siblings (a
+    busy sibling shares the core's pipelines and caches); ties: the highest id, away from
+    core 0's interrupts and housekeeping."""
+    try:
+        a = _cpu_jiffies()
+        time.sleep(window_s)
+        b = _cpu_jiffies()
+    except OSError:
+        return max(cands)
+
+    def busy(c):
+        if c not in a or c not in b:
+            return 1.0
+        dt = b[c][1] - a[c][1]
+        return (b[c][0] - a[c][0]) / dt if dt > 0 else 0.0
+    return min(cands, key=lambda c: (round(max(busy(x) for x in _siblings(c)), 2), -c))
+
+
+def core_mhz(core):
+    """Current clock of `core` (cpufreq, else /proc/cpuinfo), MHz, or None."""
+    try:
+        with open(f"/sys/devices/system/cpu/cpu{core}/cpufreq/scaling_cur_freq") as f:
+            return round(int(f.read()) / 1000.0, 1)
+    except (OSError, ValueError):
+        pass
+    try:
+        cur = None
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("processor"):
+                    cur = int(line.split(":")[1])
+                elif line.startswith("cpu MHz") and cur == core:
+                    return round(float(line.split(":")[1]), 1)
+    except (OSError, ValueError):
+        pass
+    return None
+
+
 def cpu_baseline(scene_path, size, depth):
     """The reference itself (oracle/_ref/ref_timer_d<depth>: the C/ sources built like
-    C/Makefile:4, raycast() timed alone) on the same image on one pinned host core, median of
-    3 runs (1 above 4096^2: ~40 s each); falls back to the CPU restatement
-    (oracle/build) when the reference build is absent."""
+    C/Makefile:4, raycast() timed alone) on one pinned host core, 3 runs; falls
+    back to the CPU restatement (oracle/build) when the reference build is absent.  The core is
+    the least busy of the affinity set (not core 0: interrupts and housekeeping), its clock is
+    recorded before and after every run, and min and median are reported.  Above 4096^2 the
+    sample is the same scene at 4096^2 (rays/s is per pixel; a full 8192^2 run takes ~40 s),
+    so the leg stays at ~15-30 s."""
+    n = min(size, 4096)
     ref = os.path.join(ROOT, "oracle", "_ref", f"ref_timer_d{depth}")
     if os.path.exists(ref):
-        cmd, kind = [ref, str(size), str(size), scene_path], "reference"
+        cmd, kind = [ref, str(n), str(n), scene_path], "reference"
     else:
-        cmd = [os.path.join(ROOT, "oracle", "build", "oracle_raytrace"), str(size), str(size),
+        cmd = [os.path.join(ROOT, "oracle", "build", "oracle_raytrace"), str(n), str(n),
                scene_path, "/dev/null", str(depth)]
         kind = "port"
-    runs = 3 if size <= 4096 else 1
+    runs = 3
     info = {"cpu_model": cpu_model(), "nproc": os.cpu_count()}
     try:
+        core = None
         try:
-            core = sorted(os.sched_getaffinity(0))[0]
+            core = quiet_core(sorted(os.sched_getaffinity(0)))
             cmd = ["taskset", "-c", str(core)] + cmd
         except (AttributeError, OSError):
             pass
-        res = []
+        res, mhz = [], []
         for _ in range(runs):
+            before = core_mhz(core) if core is not None else None
             out = subprocess.run(cmd, capture_output=True, text=True, timeout=300,
                                  check=True).stdout
+            mhz.append([before, core_mhz(core) if core is not None else None])
             res.append(json.loads([l for l in out.splitlines() if l.startswith("{")][-1]))
-        res.sort(key=lambda r: r["seconds"])
-        r = res[len(res) // 2]
-        return {"value": round(r["rays_per_s"], 1), "unit": "rays/s", "cores": 1, "kind": kind,
-                "sample": f"full {size}x{size} {os.path.basename(scene_path)} depth {depth} "
-                          f"render, raycast() only, 1 pinned core, median of {runs}: "
-                          f"{r['seconds']:.2f} s", **info}
+        secs = sorted(r["seconds"] for r in res)
+        med = secs[len(secs) // 2]
+        # value from the fastest run: on a shared host the slower runs measure other tenants
+        # (the same core at the same clock varied 4.6-5.9 s within one bench run)
+        return {"value": round(n * n / secs[0], 1), "unit": "rays/s", "cores": 1, "kind": kind,
+                "sample": f"full {n}x{n} {os.path.basename(scene_path)} depth {depth} render, "
+                          f"raycast() only, 1 pinned core (cpu {core}), {runs} runs: min "
+                          f"{secs[0]:.2f} s (value), median {med:.2f} s",
+                "seconds": [round(x, 3) for x in secs],
+                "value_median_time": round(n * n / med, 1),
+                "core": core, "mhz_before_after": mhz, **info}
     except Exception as e:  # noqa: BLE001
         return {"value": None, "unit": "rays/s", "cores": 1, "kind": kind,
                 "sample": f"failed: {e}", **info}
@@ -253,23 +377,28 @@ def main():
     sharded = group is not None and (mode in ("fast", "cuda") or args.shard)
     out = torch.empty((H, W, 3), dtype=torch.uint8, device="cuda")
     stream = torch.cuda.current_stream()
+    want_md5 = golden_md5(args.scene, W, H, args.depth, mode) if mode != "cuda" else None
 
     piped = parity and args.inflight == 2 and not sharded
-    if piped:   # every frame of the timed region gets its own output image
+    # every frame of the timed region gets its own output image, so that all of them can be
+    # byte-checked afterwards (the sharded step's image is the root's)
+    outs = None
+    if not sharded:
         outs = [torch.empty((H, W, 3), dtype=torch.uint8, device="cuda")
                 for _ in range(max(args.steps, 1))]
         torch.cuda.synchronize()
     frame_no = [0]
 
     def step():
-        if piped:
-            buf = outs[frame_no[0] % len(outs)]
-            frame_no[0] += 1
-            pkg.frame_submit(scene, W, H, buf.data_ptr(), depth=args.depth, mode=mode)
-        elif sharded:   # synchronous: the root holds the de-interleaved image when it returns
+        if sharded:   # synchronous: the root holds the de-interleaved image when it returns
             group.render(scene, W, H, out.data_ptr(), depth=args.depth, mode=mode)
+            return
+        buf = outs[frame_no[0] % len(outs)]
+        frame_no[0] += 1
+        if piped:
+            pkg.frame_submit(scene, W, H, buf.data_ptr(), depth=args.depth, mode=mode)
         else:
-            pkg.render_device(scene, W, H, out.data_ptr(), stream.cuda_stream, depth=args.depth,
+            pkg.render_device(scene, W, H, buf.data_ptr(), stream.cuda_stream, depth=args.depth,
                               mode=mode)
 
     def drain():
@@ -279,6 +408,7 @@ def main():
 
     pipe_tim = {}
     single = None
+    side0 = None
     if piped and not args.timed_only:
         # latency and per-phase times of a lone frame (rc_render_device, the raycast() path),
         # taken before the frame pipeline's CU-partitioned streams exist
@@ -294,11 +424,32 @@ def main():
         torch.cuda.synchronize()
         single_ms = (time.perf_counter() - ts) * 1e3 / 5
         single_phases = pkg.profile_end()
+        lone = pkg.lone_frames_check()   # every lone frame's hand-off words (7 frames)
+        md5 = pkg.p3_md5(out.cpu().numpy())
         single = {"ms": round(single_ms, 4), "value": round(W * H / (single_ms * 1e-3), 1),
-                  "note": "one frame at a time (rc_render_device); phases_ms are its phases"}
+                  "note": "one frame at a time (rc_render_device); phases_ms are its phases",
+                  "verified": f"{lone['checked'] - lone['failed']}/7 hand-offs, last image md5 "
+                              + ("== reference" if md5 == want_md5 else
+                                 "(no golden)" if want_md5 is None else "MISMATCH")}
+        # phase C after the resolver on the whole device (side=0): the pixel kernels' own
+        # time, for roofline_render (a lone frame's k_side runs beside the resolver and waits
+        # for its carry-ins, so its span is not compute time)
+        with pkg.tuned(side=0):
+            pkg.render_device(scene, W, H, out.data_ptr(), stream.cuda_stream,
+                              depth=args.depth, mode=mode)
+            torch.cuda.synchronize()
+            pkg.profile_begin()
+            for _ in range(3):
+                pkg.render_device(scene, W, H, out.data_ptr(), stream.cuda_stream,
+                                  depth=args.depth, mode=mode)
+            torch.cuda.synchronize()
+            side0 = pkg.profile_end()
+        pkg.lone_frames_check()
     for _ in range(args.warmup):
         step()
     drain()
+    if parity and not piped and not sharded:
+        pkg.lone_frames_check()   # the warmup frames: the timed region's count starts at 0
     if multi:
         dist.barrier()
     torch.cuda.synchronize()
@@ -321,6 +472,38 @@ def main():
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
     tmax = float(tmax.item())
 
+    # ---- verification of the timed frames (outside the timed region) ----
+    # hand-offs: every parity frame's latched carry hand-off words (rc_frames_wait /
+    # rc_lone_frames_check); bytes: every frame's image against frame 0's on the device, and
+    # frame 0's P3 md5 against the reference's golden
+    if piped:
+        hand = {"checked": int(pipe_tim.get("frames_checked", 0)),
+                "failed": int(pipe_tim.get("frames_failed", 0))}
+    elif parity and not sharded:
+        hand = pkg.lone_frames_check()
+    else:
+        hand = None   # no carry hand-off in this mode (sharded: checked inside each call)
+    if sharded:
+        equal, md5, gold = (1, *verify_frames(pkg, [out], want_md5)[1:]) if rank == 0 else \
+            (1, None, None)
+        nframes = 1
+    else:
+        nframes = min(args.steps, len(outs))
+        equal, md5, gold = verify_frames(pkg, outs[:nframes], want_md5)
+    ok = nframes if (equal == nframes and gold is not False and
+                     (hand is None or (hand["checked"] == args.steps and hand["failed"] == 0))) \
+        else 0
+    okt = torch.tensor([ok, nframes], dtype=torch.int64, device="cuda")
+    if multi and not sharded:
+        dist.all_reduce(okt)
+    verified = {"frames": f"{int(okt[0])}/{int(okt[1])}",
+                "bytes_equal_frame0": f"{equal}/{nframes}",
+                "frame0_md5": md5,
+                "frame0_vs_reference": ("equal" if gold else "MISMATCH" if gold is False
+                                        else "no golden for this configuration"),
+                "hand_offs": (f"{hand['checked'] - hand['failed']}/{args.steps}" if hand
+                              else "n/a")}
+
     tim = {}
     shard_stats = group.stats() if sharded else None
     if piped:
@@ -337,6 +520,7 @@ def main():
         pkg.render_device(scene, W, H, out.data_ptr(), stream.cuda_stream, depth=args.depth,
                           mode=mode, timing=tim)
     torch.cuda.synchronize()
+    line = None
     if rank == 0:
         images = 1 if sharded else world
         value = images * W * H * args.steps / tmax
@@ -348,11 +532,17 @@ def main():
                 dom_ms = pipe_tim["resolve_ms"]
             dom_flop = (work["dep_flop_per_entry"] * tim["dep_pixels"]
                         if work and tim.get("dep_pixels") else None)
-            render_ms = phases["phase_a_ms"] + phases["phase_c_ms"]
+            if side0:   # phase A + phase C (k_dep_chunks after the resolver), whole device
+                render_ms = side0["phase_a_ms"] + side0["phase_c_ms"]
+                render_kernels = "k_phase_a + k_dep_chunks (phase C after the resolver, side=0)"
+            else:
+                render_ms = phases["phase_a_ms"] + phases["phase_c_ms"]
+                render_kernels = "k_phase_a + phase C tail"
         else:
             dom_name, dom_ms = "k_render", phases["render_ms"]
             dom_flop = work["render_flop_per_px"] * W * rows_here if work else None
             render_ms = phases["render_ms"]
+            render_kernels = "k_render"
         ach = dom_flop / (dom_ms * 1e-3) / 1e12 if dom_flop and dom_ms else None
         step_ms = tmax * 1e3 / args.steps
         # per step: the dominant kernel's algorithmic work of one image over the step time
@@ -360,10 +550,11 @@ def main():
         ach_step = (dom_flop * images / world) / (step_ms * 1e-3) / 1e12 if dom_flop else None
         pmc, pmc_src = pmc_kernel(dom_name, args.scene, args.size, args.depth, mode)
         store_name = "k_phase_a" if parity else "k_render"   # the framebuffer's writer
-        spmc, _ = pmc_kernel(store_name, args.scene, args.size, args.depth, mode)
+        spmc, spmc_src = pmc_kernel(store_name, args.scene, args.size, args.depth, mode)
         store_ms = phases["phase_a_ms"] if parity else phases["render_ms"]
         rach = (work["render_flop_per_px"] * W * rows_here / (render_ms * 1e-3) / 1e12
                 if work and render_ms else None)
+        fb_bytes = 3 * W * rows_here
         line = {
             "metric": ("primary rays/sec (= pixels/sec) at 4096x4096, quadric.scene"
                        if (args.scene, W) == ("quadric", 4096) else
@@ -387,6 +578,7 @@ def main():
                                        "(rc_render_sharded)" if sharded else
                                        (f"replicas x{world}" if world > 1 else "single GPU")),
                        "frames_in_flight": 2 if piped else 1},
+            "verified": verified,
             "phases_ms": {k: round(v, 4) for k, v in phases.items() if k.endswith("_ms")},
             "tuning": ({t.split("=", 1)[0]: int(t.split("=", 1)[1]) for t in args.tune}
                        if args.tune else "default"),
@@ -405,23 +597,28 @@ def main():
                          "note": ("serial carry chain: latency-bound, see DESIGN.md; frac = per "
                                   "launch, frac_per_step = one image's work over ms_per_step"
                                   if parity else "throughput kernel")},
-            "roofline_render": {"bound": "valu",
-                                "kernel": "k_phase_a+k_phase_c" if parity else "k_render",
+            "roofline_render": {"bound": "valu", "kernel": render_kernels,
                                 "kernel_ms": round(render_ms, 4),
                                 "achieved": round(rach, 3) if rach else None,
                                 "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
                                 "frac": round(rach / PEAK_FP64_TFLOPS, 4) if rach else None},
-            # the framebuffer store: its writer kernel's HBM write bytes (PMC WRITE_SIZE, which
-            # for phase A also holds the classes, writer carries and DEP records) over that
-            # kernel's time; the algorithmic 3 B/pixel beside it
-            "roofline_hbm": {"bound": "hbm", "kernel": store_name + " (framebuffer store)",
-                             "achieved": (round(spmc["write_bytes"] / (store_ms * 1e-3) / 1e9, 3)
-                                          if spmc and spmc.get("write_bytes") and store_ms
-                                          else None),
-                             "algorithmic": (round(3 * W * rows_here / (store_ms * 1e-3) / 1e9, 3)
-                                             if store_ms else None),
+            # the framebuffer store (north_star): its 3 B/pixel over the writer kernel's time.
+            # In parity the writer (k_phase_a) also writes the classes, writer carries and
+            # DEP records; its whole PMC WRITE_SIZE is reported beside, labelled as such.
+            "roofline_hbm": {"bound": "hbm", "kernel": store_name,
+                             "what": "framebuffer store (3 B/pixel RGB) over the writer's time",
+                             "achieved": (round(fb_bytes / (store_ms * 1e-3) / 1e9, 3)
+                                          if store_ms else None),
                              "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                             "write_bytes_pmc": spmc["write_bytes"] if spmc else None},
+                             "frac": (round(fb_bytes / (store_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 5)
+                                      if store_ms else None),
+                             "framebuffer_bytes": fb_bytes,
+                             "kernel_ms": round(store_ms, 4) if store_ms else None,
+                             "kernel_write_bytes_pmc": spmc["write_bytes"] if spmc else None,
+                             "kernel_write_gbs_pmc": (
+                                 round(spmc["write_bytes"] / (store_ms * 1e-3) / 1e9, 3)
+                                 if spmc and spmc.get("write_bytes") and store_ms else None),
+                             "pmc_source": spmc_src},
         }
         if single:
             line["single_frame"] = single
@@ -437,21 +634,10 @@ def main():
     # N>1 parity replicas: the sharded single image as well, reported beside (never as) value.
     # It is the only multi-process RCCL exchange of the run, so a watchdog bounds it: if it has
     # not finished in LEG_TIMEOUT_S, rank 0 prints the line with the leg marked as timed out
-    # and every rank exits (the timed region's result is never lost to a stuck exchange).
+    # and every rank exits with LEG_TIMEOUT_EXIT.
     LEG_TIMEOUT_S = 120
-    leg_done = threading.Event()
 
-    def leg_watchdog():
-        if leg_done.wait(LEG_TIMEOUT_S):
-            return
-        if rank == 0:
-            line["sharded_single_image"] = {"error": f"timed out after {LEG_TIMEOUT_S} s"}
-            print(json.dumps(line), flush=True)
-        os._exit(0)
-
-    shard_leg = None
-    if group is not None and not sharded and not args.timed_only:
-        threading.Thread(target=leg_watchdog, daemon=True).start()
+    def shard_leg():
         dist.barrier()
         group.render(scene, W, H, out.data_ptr(), depth=args.depth, mode=mode)   # warm
         dist.barrier()
@@ -462,22 +648,37 @@ def main():
         dist.barrier()
         ms = (time.perf_counter() - ts) * 1e3 / reps
         st = group.stats()
-        shard_leg = {"value": round(W * H / (ms * 1e-3), 1), "unit": "rays/s", "ms": round(ms, 4),
-                     "note": f"one {W}x{H} image row-sharded over {world} GPUs (rc_render_sharded: "
-                             "phase A on every rank, DEP entries gathered to rank 0 over RCCL, "
-                             "serial carry resolver there, carry-ins back, phase C on every rank, "
-                             "row blocks gathered); strong scaling, capped by the resolver",
-                     "stats": {k: (round(v, 4) if isinstance(v, float) else v)
-                               for k, v in (st or {}).items()}}
-    leg_done.set()
+        leg = {"value": round(W * H / (ms * 1e-3), 1), "unit": "rays/s", "ms": round(ms, 4),
+               "note": f"one {W}x{H} image row-sharded over {world} GPUs (rc_render_sharded: "
+                       "phase A on every rank, DEP entries gathered to rank 0 over RCCL, "
+                       "serial carry resolver there, carry-ins back, phase C on every rank, "
+                       "row blocks gathered); strong scaling, capped by the resolver",
+               "stats": {k: (round(v, 4) if isinstance(v, float) else v)
+                         for k, v in (st or {}).items()}}
+        if rank == 0:
+            m = pkg.p3_md5(out.cpu().numpy())
+            leg["md5_vs_reference"] = ("equal" if m == want_md5 else "no golden"
+                                       if want_md5 is None else "MISMATCH")
+        return leg
+
+    def leg_timed_out():
+        if rank == 0:
+            line["sharded_single_image"] = {"error": f"timed out after {LEG_TIMEOUT_S} s"}
+            print(json.dumps(line), flush=True)
+
+    shard_leg_res = None
+    if group is not None and not sharded and not args.timed_only:
+        shard_leg_res = run_leg_with_watchdog(shard_leg, LEG_TIMEOUT_S, leg_timed_out)
     if rank == 0:
-        if shard_leg:
-            line["sharded_single_image"] = shard_leg
+        if shard_leg_res:
+            line["sharded_single_image"] = shard_leg_res
         print(json.dumps(line), flush=True)
     if group is not None:
         group.close()
     if multi:
         dist.destroy_process_group()
+    if verified["frames"].split("/")[0] != verified["frames"].split("/")[1]:
+        sys.exit(4)   # a timed frame failed its checks: the line is printed, the run fails
 
 
 if __name__ == "__main__":

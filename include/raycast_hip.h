@@ -148,6 +148,10 @@ typedef struct rc_timing {
   double d2h_ms;         /* device -> host copy of the pixmap                          */
   int64_t dep_pixels;    /* parity: pixels whose first reflection missed               */
   int64_t zero_normalize;/* count of zero-length normalize events (C/v3math.c:183-187) */
+  int64_t frames_checked;/* parity frames whose hand-off words were read back: rc_frames_wait
+                            (every frame since the previous wait), rc_render_device with
+                            timing (1)                                                  */
+  int64_t frames_failed; /* of them, frames whose carry hand-off failed (image invalid)  */
 } rc_timing;
 
 /* Fill *opt with the defaults (then the RAYCAST_* environment overrides if use_env). */
@@ -190,6 +194,19 @@ int rc_render_device(const rc_scene *scene, int width, int height, int row0, int
 int rc_frame_submit(const rc_scene *scene, int width, int height, const rc_options *opt,
                     uint8_t *d_out);
 int rc_frames_wait(rc_timing *timing);
+/* Every parity frame is verified: after its last kernel the words its bounded carry
+ * hand-offs set on a failure (timed-out spin: code, workgroup, details) are copied on the
+ * frame's own stream into a pinned per-frame ring, before the frame's workspace can be reused.
+ * rc_frames_wait reads back every frame since the previous wait (frames_checked /
+ * frames_failed in *timing) and returns -1 if any failed; rc_frame_submit refuses new frames
+ * once a frame in flight is known to have failed.  One-frame-at-a-time renders
+ * (rc_render_device, rc_render) are read back at the next call on the device (which then
+ * returns -1) or by rc_lone_frames_check, which synchronises the current device and returns
+ * the count since its previous call (-1 if any failed). */
+int rc_lone_frames_check(int64_t *checked, int64_t *failed);
+/* Test aid: the nth_frame-th parity frame from now (0 = the next, any entry point, any
+ * device) fails its hand-off as a timed-out spin would (error code 4); -1 cancels. */
+int rc_debug_inject_error(int nth_frame);
 /* Wait for every submitted frame, then release the current device's frame pipeline (its
  * CU-partitioned streams and events; the frame workspaces stay allocated).  The next
  * rc_frame_submit builds it again, re-reading RC_PIPE_* from the environment.  Returns what

@@ -56,6 +56,13 @@ class JsonDataT(ctypes.Structure):
                 ("num_shapes", ctypes.c_int), ("num_lights", ctypes.c_int)]
 
 
+class PPMFormat(ctypes.Structure):
+    """PPMFormat, C/ppm.h:6-12."""
+    _fields_ = [("width", ctypes.c_int), ("height", ctypes.c_int), ("size", ctypes.c_int),
+                ("maxColor", ctypes.c_uint8), ("depth", ctypes.c_uint8),
+                ("tupleType", ctypes.c_char_p), ("pixmap", ctypes.c_void_p)]
+
+
 class RcOptions(ctypes.Structure):
     _fields_ = [("max_recursion", ctypes.c_int), ("mode", ctypes.c_int),
                 ("num_gpus", ctypes.c_int), ("device", ctypes.c_int)]
@@ -64,7 +71,8 @@ class RcOptions(ctypes.Structure):
 class RcTiming(ctypes.Structure):
     _fields_ = [("total_ms", ctypes.c_double), ("kernel_ms", ctypes.c_double),
                 ("resolve_ms", ctypes.c_double), ("d2h_ms", ctypes.c_double),
-                ("dep_pixels", ctypes.c_int64), ("zero_normalize", ctypes.c_int64)]
+                ("dep_pixels", ctypes.c_int64), ("zero_normalize", ctypes.c_int64),
+                ("frames_checked", ctypes.c_int64), ("frames_failed", ctypes.c_int64)]
 
 
 class RcPhaseStats(ctypes.Structure):
@@ -104,7 +112,8 @@ HIP_EXPORTS = ["raycast", "rc_default_options", "rc_scene_create", "rc_scene_des
                "rc_frames_wait", "rc_pipe_reset", "rc_group_unique_id", "rc_group_create_rank",
                "rc_group_create_local", "rc_group_destroy", "rc_group_size",
                "rc_group_transport", "rc_render_sharded", "rc_group_last_stats",
-               "rc_default_tuning", "rc_set_tuning", "rc_get_tuning"]
+               "rc_default_tuning", "rc_set_tuning", "rc_get_tuning", "rc_lone_frames_check",
+               "rc_debug_inject_error"]
 FRONT_EXPORTS = ["add_new_sphere", "add_new_plane", "add_new_quadric", "free_shape_list",
                  "free_light_list", "add_new_spot_light", "add_new_point_light", "parse_json",
                  "set_to_black", "ppm_WriteOutP3", "ppm_clamp"]
@@ -129,7 +138,12 @@ def front_lib():
     lib.free_shape_list.restype = ctypes.c_void_p
     lib.free_light_list.argtypes = [ctypes.c_void_p]
     lib.free_light_list.restype = ctypes.c_void_p
+    lib.ppm_WriteOutP3.argtypes = [PPMFormat, ctypes.c_void_p]
+    lib.ppm_WriteOutP3.restype = None
     return lib
+
+
+_torch_tried = False
 
 
 def _one_hip_runtime():
@@ -140,8 +154,10 @@ def _one_hip_runtime():
     teardown corrupts the heap at exit).  Importing torch first makes libraycast_hip.so's
     `libamdhip64.so.7` / `librccl.so.1` resolve to the runtime already loaded: one per
     process.  Without torch, /opt/rocm's runtime is the only one."""
-    if "torch" in sys.modules:
+    global _torch_tried
+    if _torch_tried or "torch" in sys.modules:
         return
+    _torch_tried = True   # once: a failed import is not retried on every call
     try:
         import torch  # noqa: F401
     except ImportError:
@@ -149,6 +165,7 @@ def _one_hip_runtime():
 
 
 _HIP_LOCK = threading.Lock()
+_hip = None
 
 
 def hip_lib():
@@ -156,11 +173,18 @@ def hip_lib():
     # Under a lock: threads making their first call at once must not load the library while
     # another is still importing torch (a half-imported torch is already in sys.modules, and
     # the library would then map /opt/rocm's HIP runtime beside torch's: _one_hip_runtime).
+    # Once bound, later calls take the cached handle without the lock.
+    lib = _hip
+    if lib is not None:
+        return lib
     with _HIP_LOCK:
         return _hip_lib_locked()
 
 
 def _hip_lib_locked():
+    global _hip
+    if _hip is not None:
+        return _hip
     _one_hip_runtime()
     lib = _load(os.environ.get("RC_HIP_LIB", "libraycast_hip.so"))
     lib.rc_scene_create.argtypes = [ctypes.POINTER(JsonDataT)]
@@ -197,6 +221,10 @@ def _hip_lib_locked():
     lib.rc_get_tuning.argtypes = [ctypes.POINTER(RcTuning)]
     lib.rc_get_tuning.restype = None
     lib.rc_set_tuning.argtypes = [ctypes.POINTER(RcTuning)]
+    lib.rc_lone_frames_check.argtypes = [ctypes.POINTER(ctypes.c_int64),
+                                         ctypes.POINTER(ctypes.c_int64)]
+    lib.rc_debug_inject_error.argtypes = [ctypes.c_int]
+    _hip = lib
     return lib
 
 
@@ -204,6 +232,9 @@ _libc = ctypes.CDLL(None)
 _libc.fopen.restype = ctypes.c_void_p
 _libc.fopen.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
 _libc.fclose.argtypes = [ctypes.c_void_p]
+_libc.open_memstream.restype = ctypes.c_void_p
+_libc.open_memstream.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t)]
+_libc.free.argtypes = [ctypes.c_void_p]
 
 
 _PACK_LOCK = threading.Lock()
@@ -377,9 +408,69 @@ def frames_wait(timing=None):
     """Block until every submitted frame is complete (rc_frames_wait)."""
     t = RcTiming()
     if hip_lib().rc_frames_wait(ctypes.byref(t)) != 0:
-        raise RuntimeError("rc_frames_wait failed: a resolver hand-off timed out (see stderr)")
+        raise RuntimeError(f"rc_frames_wait failed: {t.frames_failed} of {t.frames_checked} "
+                           "frames' carry hand-offs failed (see stderr)")
     if timing is not None:
         timing.update({k: getattr(t, k) for k, _ in RcTiming._fields_})
+
+
+def lone_frames_check():
+    """Synchronise the device and read back every one-frame-at-a-time parity frame's hand-off
+    words since the previous check (rc_lone_frames_check): {"checked": n, "failed": 0}; raises
+    if a frame failed."""
+    c, f = ctypes.c_int64(0), ctypes.c_int64(0)
+    rc = hip_lib().rc_lone_frames_check(ctypes.byref(c), ctypes.byref(f))
+    if rc != 0:
+        raise RuntimeError(f"rc_lone_frames_check: {f.value} of {c.value} frames failed (see stderr)")
+    return {"checked": c.value, "failed": f.value}
+
+
+def inject_error(nth_frame):
+    """Test aid (rc_debug_inject_error): the nth_frame-th parity frame from now (0 = next)
+    fails its carry hand-off as a timed-out spin would; -1 cancels."""
+    if hip_lib().rc_debug_inject_error(int(nth_frame)) != 0:
+        raise ValueError(nth_frame)
+
+
+def write_p3(img, path):
+    """ppm_WriteOutP3 (C/ppm.c:168-184, the product's byte-identical writer) of an [H, W, 3]
+    uint8 image into `path`."""
+    lib = front_lib()
+    h, w, _ = img.shape
+    img = np.ascontiguousarray(img)
+    p = PPMFormat(w, h, w * h * 3, 255, 0, None, img.ctypes.data)
+    f = _libc.fopen(os.fsencode(path), b"wb")
+    if not f:
+        raise OSError(path)
+    try:
+        lib.ppm_WriteOutP3(p, ctypes.c_void_p(f))
+    finally:
+        _libc.fclose(f)
+
+
+def p3_bytes(img):
+    """The P3 file the reference would write for img (C/ppm.c:168-184), produced by the
+    product writer into memory (open_memstream)."""
+    lib = front_lib()
+    h, w, _ = img.shape
+    img = np.ascontiguousarray(img)
+    p = PPMFormat(w, h, w * h * 3, 255, 0, None, img.ctypes.data)
+    buf, size = ctypes.c_void_p(), ctypes.c_size_t()
+    f = _libc.open_memstream(ctypes.byref(buf), ctypes.byref(size))
+    if not f:
+        raise MemoryError("open_memstream")
+    lib.ppm_WriteOutP3(p, ctypes.c_void_p(f))
+    _libc.fclose(f)
+    try:
+        return ctypes.string_at(buf, size.value)
+    finally:
+        _libc.free(buf)
+
+
+def p3_md5(img):
+    """md5 of the P3 file the reference would write for img (C/ppm.c:168-184)."""
+    import hashlib
+    return hashlib.md5(p3_bytes(img)).hexdigest()
 
 
 def pipe_reset():

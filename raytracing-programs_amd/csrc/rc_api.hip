@@ -9,6 +9,7 @@
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <condition_variable>
@@ -65,8 +66,84 @@ rc_tuning default_tuning() {
   return t;
 }
 rc_tuning g_tune = default_tuning();
-const rc_tuning& tune() { return g_tune; }
+std::mutex g_tune_mu;   // rc_set_tuning writes g_tune while render threads read it
+rc_tuning tune() {
+  std::lock_guard<std::mutex> lk(g_tune_mu);
+  return g_tune;
+}
 double g_last_kernel_ms = 0.0;
+std::atomic<int> g_pool_threads{-1};   // copy_threads the host pool was built with (-1: not yet)
+// rc_debug_inject_error: the parity frame (counted from the call, any path) whose resolver
+// raises its error word; -1 = off
+std::atomic<int> g_inject{-1};
+int take_inject() {
+  int v = g_inject.load();
+  while (v >= 0 && !g_inject.compare_exchange_weak(v, v - 1)) {
+  }
+  return v == 0 ? 1 : 0;
+}
+
+const char* spin_site(int code) {
+  static const char* site[] = {"", "team granule", "phase-C carry-in", "helper queue",
+                               "injected (rc_debug_inject_error)"};
+  return code >= 1 && code <= 4 ? site[code] : "?";
+}
+
+int FrameLog::enqueue(const void* team, hipStream_t st) {
+  if (!ring) {
+    HIP_TRY(hipHostMalloc((void**)&ring, kRing * sizeof(Entry), hipHostMallocDefault));
+    for (int i = 0; i < kRing; ++i) ring[i].code = kPending;
+  }
+  if (head - tail >= kRing) {   // every entry still unread: wait for the frames, read them
+    HIP_TRY(hipDeviceSynchronize());
+    if (drain() < 0) return -1;
+  }
+  Entry* e = &ring[head % kRing];
+  ((volatile Entry*)e)->code = kPending;
+  HIP_TRY(hipMemcpyAsync(e, team, sizeof(Entry), hipMemcpyDeviceToHost, st));
+  ++head;
+  return 0;
+}
+
+long long FrameLog::poll() {
+  long long found = 0;
+  while (tail < head) {
+    volatile Entry* e = &ring[tail % kRing];
+    const int code = e->code;
+    if (code == kPending) break;
+    if (code != 0) {
+      ++found;
+      std::fprintf(stderr,
+                   "Error: parity frame %lld (%s) is invalid: its hand-off failed (code %d: %s) "
+                   "at workgroup %d, detail %d/%d\n",
+                   tail, what, code, spin_site(code), e->block, e->info, e->info2);
+    }
+    e->code = kPending;
+    ++tail;
+    ++checked;
+  }
+  failed += found;
+  return found;
+}
+
+long long FrameLog::drain() {
+  long long found = poll();
+  if (tail < head) {
+    std::fprintf(stderr, "Error: %lld parity frame(s) (%s) were never verified (their hand-off "
+                 "words did not arrive after a synchronisation)\n", head - tail, what);
+    found += head - tail;
+    failed += head - tail;
+    checked += head - tail;
+    tail = head;
+  }
+  return found;
+}
+
+void FrameLog::take(long long* c, long long* f) {
+  if (c) *c = checked;
+  if (f) *f = failed;
+  checked = failed = 0;
+}
 
 int ctx_get(int device, DevCtx** out) {
   if (device < 0 || device >= kMaxDevices) return -1;
@@ -81,6 +158,9 @@ int ctx_get(int device, DevCtx** out) {
     for (auto& set : c.ev)
       for (auto& e : set) HIP_TRY(hipEventCreate(&e));
     if (c.fb.zcount.ensure(64)) return -1;
+    HIP_TRY(hipEventCreateWithFlags(&c.ws_ev, hipEventDisableTiming));
+    c.lone_log.what = "one frame at a time";
+    c.pipe.log.what = "frames in flight";
     c.device = device;
     c.init = true;
   }
@@ -128,6 +208,7 @@ class HostPool {
 
  private:
   HostPool() {
+    g_pool_threads = tune().copy_threads;
     int t = tune().copy_threads - 1;
     if (t < 0) t = 0;
     if (t > 31) t = 31;
@@ -271,7 +352,7 @@ void rc_default_tuning(rc_tuning* t) {
 }
 
 void rc_get_tuning(rc_tuning* t) {
-  if (t) *t = g_tune;
+  if (t) *t = tune();
 }
 
 int rc_set_tuning(const rc_tuning* t) {
@@ -293,6 +374,23 @@ int rc_set_tuning(const rc_tuning* t) {
     std::fprintf(stderr, "Error: rc_set_tuning: a field is out of range\n");
     return -1;
   }
+  // fields read once: the host pool's size at its first use, the frame pipeline's layout at
+  // its build (rc_pipe_reset rebuilds it)
+  const int pool = g_pool_threads.load();
+  if (pool >= 0 && t->copy_threads != pool)
+    std::fprintf(stderr, "Warning: rc_set_tuning: copy_threads is fixed at the host pool's "
+                 "first use (%d threads); the new value is ignored\n", pool);
+  for (auto& c : g_ctx) {
+    if (!c.pipe.init) continue;
+    if (t->pipe_resolvers != c.pipe.built_lanes || t->pipe_slots != c.pipe.built_slots ||
+        t->pipe_res_cus != c.pipe.built_res || (t->pipe_timing != 0) != c.pipe.rt_on ||
+        (t->pipe_slotstreams == 0) != c.pipe.fifo) {
+      std::fprintf(stderr, "Warning: rc_set_tuning: the pipe_* fields take effect when device "
+                   "%d's frame pipeline is rebuilt (rc_pipe_reset)\n", c.device);
+      break;
+    }
+  }
+  std::lock_guard<std::mutex> lk(g_tune_mu);
   g_tune = *t;
   return 0;
 }
@@ -414,7 +512,7 @@ int ensure_parity(DevCtx& c, FrameBufs& b, int W, int H, rc::ParityWork& w, int 
   // the longest segments outnumber one-per-CU's waves and the chains that start late set the
   // resolver's time (measured: 4.9e9 -> 5.4e9 rays/s with frames in flight, 6.37 -> 6.49 ms
   // for a lone frame).
-  const rc_tuning& tu = tune();
+  const rc_tuning tu = tune();
   const int one_per_cu = tu.resolve_shared ? 0 : 1;
   int lds = !one_per_cu ? 0 : piped ? 56 * 1024 : 96 * 1024;
   if (tu.resolve_lds_kb > 0) lds = tu.resolve_lds_kb * 1024;
@@ -532,10 +630,28 @@ int ensure_parity(DevCtx& c, FrameBufs& b, int W, int H, rc::ParityWork& w, int 
   return 0;
 }
 
-// Enqueue one render of rows (row0 + k*row_step) into d_out on c.stream.
+int enqueue_render_ws(DevCtx& c, const rc_scene* s, int W, int H, int row0, int row_step,
+                      int nrows, const rc_options* opt, uint8_t* d_out, hipStream_t stream,
+                      bool timed, uint32_t* patch, hipEvent_t** evset);
+
+// Enqueue one render of rows (row0 + k*row_step) into d_out on `stream`, using the device's
+// one-frame workspace c.fb: after the previous render that used it, whatever its stream.
 int enqueue_render(DevCtx& c, const rc_scene* s, int W, int H, int row0, int row_step, int nrows,
                    const rc_options* opt, uint8_t* d_out, hipStream_t stream, bool timed,
                    uint32_t* patch = nullptr, hipEvent_t** evset = nullptr) {
+  if (c.ws_valid && c.ws_stream != stream) HIP_TRY(hipStreamWaitEvent(stream, c.ws_ev, 0));
+  const int rc = enqueue_render_ws(c, s, W, H, row0, row_step, nrows, opt, d_out, stream, timed,
+                                   patch, evset);
+  // recorded even after a failed enqueue: whatever was enqueued stays ordered
+  HIP_TRY(hipEventRecord(c.ws_ev, stream));
+  c.ws_stream = stream;
+  c.ws_valid = true;
+  return rc;
+}
+
+int enqueue_render_ws(DevCtx& c, const rc_scene* s, int W, int H, int row0, int row_step,
+                      int nrows, const rc_options* opt, uint8_t* d_out, hipStream_t stream,
+                      bool timed, uint32_t* patch, hipEvent_t** evset) {
   rc::LaunchScene ls;
   if (upload_scene(c.fb, stream, s, ls)) return -1;
   unsigned long long* zc = (unsigned long long*)c.fb.zcount.p;
@@ -570,8 +686,9 @@ int enqueue_render(DevCtx& c, const rc_scene* s, int W, int H, int row0, int row
   }
   if (w.split_shade) ls.dep_fast = 0;   // k_classify leaves no primary shade
   w.patch = patch;
+  w.inject = take_inject();
   HIP_TRY(rc::launch_parity(ls, W, H, maxrec, d_out, w, zc, stream, timed ? ev + 1 : nullptr));
-  return 0;
+  return c.lone_log.enqueue(w.team, stream);
 }
 
 // After a synchronised parity render: the resolver's and phase C's bounded spins set
@@ -583,7 +700,6 @@ int report_spin_error(const FrameBufs& b, const char* where) {
   int e[4] = {0, 0, 0, 0};
   if (hipMemcpy(e, b.team.p, sizeof e, hipMemcpyDeviceToHost) != hipSuccess) return -1;
   if (!e[0]) return 0;
-  static const char* site[] = {"", "team granule", "phase-C carry-in", "helper queue"};
   int dq[3] = {0, 0, 0}, cnt[16] = {};
   (void)hipMemcpy(dq, (const char*)b.team.p + rc::team_dq_offset(), sizeof dq,
                   hipMemcpyDeviceToHost);
@@ -592,7 +708,7 @@ int report_spin_error(const FrameBufs& b, const char* where) {
                "Error: parity resolver hand-off timed out (code %d: %s; %s) at workgroup %d, "
                "detail %d/%d; segments %d, DEP entries %d, resolver census %d, helper queue "
                "prod %d claim %d finished %d, side workgroups go %d gave-up %d\n",
-               e[0], e[0] >= 1 && e[0] <= 3 ? site[e[0]] : "?", where, e[1], e[2], e[3], cnt[0],
+               e[0], spin_site(e[0]), where, e[1], e[2], e[3], cnt[0],
                cnt[2], cnt[5], dq[0], dq[1], dq[2], cnt[12], cnt[13]);
   const int nseg = cnt[0], ndep = cnt[2];
   if (nseg > 0 && ndep > 0 && b.cin.p && b.seg_start.p) {
@@ -739,6 +855,12 @@ int rc_render_device(const rc_scene* s, int W, int H, int row0, int row_step, in
   DevCtx* c;
   if (ctx_get(dev, &c)) return -1;
   std::lock_guard<std::mutex> lk(c->mu);
+  // an earlier frame of this workspace whose hand-off failed is reported by the next call
+  // (once: the report consumes the counts)
+  if (c->lone_log.poll() > 0) {
+    c->lone_log.take(nullptr, nullptr);
+    return -1;
+  }
   hipStream_t st = stream ? (hipStream_t)stream : c->stream;
   // the scene upload and events live on the ctx stream: order them with the caller's stream
   if (st != c->stream) {
@@ -753,7 +875,13 @@ int rc_render_device(const rc_scene* s, int W, int H, int row0, int row_step, in
   if (timing) {
     std::memset(timing, 0, sizeof *timing);
     HIP_TRY(hipStreamSynchronize(st));
+    const long long before = c->lone_log.checked;
+    if (c->lone_log.poll() > 0) {
+      c->lone_log.take(nullptr, nullptr);
+      return -1;
+    }
     if (check_spin_error(c->fb, opt)) return -1;
+    timing->frames_checked = c->lone_log.checked - before;
     fill_device_timing(*c, opt, timing);
     timing->total_ms = timing->kernel_ms;
   }
@@ -819,7 +947,7 @@ int pipe_init(DevCtx& c, long long pixels) {
   // phases are the bound (reflection 2048^2 d4 6.9e9 -> 7.9e9, simple 1024^2 d6 3.5e9 -> 3.7e9
   // rays/s vs half); half up to 32 Mpixel (quadric 4096^2: 5.7e9 at 128 CUs, 5.1e9 at 112);
   // 3/8 above (quadric 8192^2: 7.4e9 at 96 CUs, 6.4e9 at 128, 6.0e9 at 80).
-  const rc_tuning& tu = tune();
+  const rc_tuning tu = tune();
   int res = pixels < (8ll << 20) ? c.cus / 4 : pixels < (32ll << 20) ? c.cus / 2 : c.cus * 3 / 8;
   if (tu.pipe_res_cus > 0) res = tu.pipe_res_cus;
   p.lanes = tu.pipe_resolvers;
@@ -861,6 +989,9 @@ int pipe_init(DevCtx& c, long long pixels) {
     HIP_TRY(hipEventCreate(&e[1]));
   }
   p.res_cus = res;
+  p.built_lanes = tu.pipe_resolvers;
+  p.built_slots = tu.pipe_slots;
+  p.built_res = tu.pipe_res_cus;
   p.init = true;
   return 0;
 }
@@ -884,6 +1015,13 @@ int rc_frame_submit(const rc_scene* s, int W, int H, const rc_options* opt, uint
   }
   if (pipe_init(*c, (long long)W * H)) return -1;
   Pipe& p = c->pipe;
+  // fail fast: a frame in flight whose hand-off already failed (its entry has arrived)
+  p.log.poll();
+  if (p.log.failed > 0) {
+    std::fprintf(stderr, "Error: rc_frame_submit: %lld frame(s) in flight failed; call "
+                 "rc_frames_wait\n", p.log.failed);
+    return -1;
+  }
   const int k = (int)(p.total % p.slots);
   const int lane = (int)(p.total % p.lanes);
   FrameBufs& b = p.fb[k];
@@ -913,11 +1051,16 @@ int rc_frame_submit(const rc_scene* s, int W, int H, const rc_options* opt, uint
   const int e = (int)(p.submitted % Pipe::kEv);
   w.rt0 = p.rt_on ? p.rt[e][0] : nullptr;
   w.rt1 = p.rt_on ? p.rt[e][1] : nullptr;
+  w.inject = take_inject();
   HIP_TRY(rc::launch_parity(ls, W, H, maxrec, d_out, w, zc, st, nullptr));
   if (p.fifo) {   // phase C on the lane's stream, after the resolver
     HIP_TRY(rc::launch_phase_c(ls, W, H, maxrec, d_out, w, zc, p.pc[lane]));
+    // the frame's hand-off words, before the event that lets slot k's next frame reset them
+    if (p.log.enqueue(w.team, p.pc[lane])) return -1;
     HIP_TRY(hipEventRecord(p.cdone[k], p.pc[lane]));
     p.cpend[k] = true;
+  } else if (p.log.enqueue(w.team, st)) {   // slot streams: the frame ends on its slot's stream
+    return -1;
   }
   p.submitted++;
   p.frames++;
@@ -944,7 +1087,15 @@ int rc_frames_wait(rc_timing* timing) {
     for (int r = 0; r < p.lanes; ++r)
       if (p.pc[r]) HIP_TRY(hipStreamSynchronize(p.pc[r]));
     for (int k = 0; k < p.slots; ++k) p.cpend[k] = false;
-    for (int k = 0; k < p.slots; ++k) {   // the last frame of each slot
+    // every frame since the last wait, from its latched hand-off words (FrameLog)
+    if (p.log.drain() > 0) rc = -1;
+    long long checked = 0, failed = 0;
+    p.log.take(&checked, &failed);
+    if (timing) {
+      timing->frames_checked = checked;
+      timing->frames_failed = failed;
+    }
+    for (int k = 0; k < p.slots; ++k) {   // the last frame of each slot, with the details
       if (!p.used[k] || !p.fb[k].team.p) continue;
       if (report_spin_error(p.fb[k], "frames in flight")) rc = -1;
     }
@@ -978,6 +1129,27 @@ int rc_pipe_reset(void) {
   std::lock_guard<std::mutex> lk(c->mu);
   pipe_release(*c);
   return rc;
+}
+
+int rc_lone_frames_check(int64_t* checked, int64_t* failed) {
+  int dev = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  DevCtx* c;
+  if (ctx_get(dev, &c)) return -1;
+  HIP_TRY(hipDeviceSynchronize());   // the frames ran on the callers' streams
+  std::lock_guard<std::mutex> lk(c->mu);
+  c->lone_log.drain();
+  long long ch = 0, f = 0;
+  c->lone_log.take(&ch, &f);
+  if (checked) *checked = ch;
+  if (failed) *failed = f;
+  return f ? -1 : 0;
+}
+
+int rc_debug_inject_error(int nth_frame) {
+  if (nth_frame < -1) return -1;
+  g_inject = nth_frame;
+  return 0;
 }
 
 int rc_profile_begin(void) {
@@ -1094,7 +1266,14 @@ int rc_render(const rc_scene* s, int W, int H, const rc_options* opt, uint8_t* p
   } else if (copy_to_host(*c, pixmap, d_out, (size_t)H * row_bytes, c->stream)) {
     return -1;
   }
-  if (check_spin_error(c->fb, opt)) return -1;
+  // this frame's latched hand-off words (and any earlier frame's still unread); a failure is
+  // reported by this call and consumed
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  if (c->lone_log.poll() > 0) {
+    (void)check_spin_error(c->fb, opt);   // the details, while the workspace still holds them
+    c->lone_log.take(nullptr, nullptr);
+    return -1;
+  }
   if (timing) {
     fill_device_timing(*c, opt, timing);
     timing->d2h_ms =

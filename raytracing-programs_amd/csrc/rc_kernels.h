@@ -69,6 +69,7 @@ struct ParityWork {
   uint32_t* patch;          // optional [P] packed RGB of DEP entry j (rc_render's overlapped copy)
   int defer_c;              // pipelined: launch_parity stops after the resolver; phase C is
                             // enqueued later by launch_phase_c (after rdone)
+  int inject;               // test aid: the resolver raises its error word (code 4) at start
 };
 
 constexpr int kSegOrderMax = 65536;   // segments ordered for the resolver queue (else FIFO)

@@ -1225,10 +1225,13 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
     int* __restrict__ counters, int* __restrict__ head,
     CinG* __restrict__ cin, int team_blocks, int long_len, TeamState* __restrict__ ts,
     unsigned* __restrict__ trace, int G, int wave_k, int resolve_k, unsigned tag,
-    int helpers, int hand_run) {
+    int helpers, int hand_run, int inject) {
   // census for phase C's side kernel: it only proceeds once every resolver block is resident
   if (threadIdx.x == 0)
     __hip_atomic_fetch_add(&counters[5], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // test aid (rc_debug_inject_error): this frame's hand-off fails as a timed-out spin would
+  // (first writer wins; every spin of the frame then gives up at its next check)
+  if (inject && blockIdx.x == 0 && threadIdx.x == 0) set_error(ts, 4, 0, 0);
   const int nseg = counters[0];
   const int ndep = counters[2];
   const bool ordered = counters[3] != 0;
@@ -2184,7 +2187,7 @@ hipError_t launch_parity(const LaunchScene& s, int W, int H, int maxrec, uint8_t
                      maxrec, (const DepRec*)w.deprec, w.dep_pix, w.seg_key, w.wcarry,
                      w.seg_start, w.seg_order, w.counters, w.counters + 1, (CinG*)w.cin, w.team_blocks,
                      w.long_len, (TeamState*)w.team, w.trace, w.coop_group, w.wave_k,
-                     w.resolve_k, w.epoch, w.helpers, w.hand_run);
+                     w.resolve_k, w.epoch, w.helpers, w.hand_run, w.inject);
   if (w.rstream) {
     if (w.rt1) (void)hipEventRecord(w.rt1, rs);
     (void)hipEventRecord(w.rdone, rs);
@@ -2353,7 +2356,7 @@ hipError_t launch_shard_resolve(const LaunchScene& s, int W, int H, int G, int r
                      sc, maxrec, (const DepRec*)w.deprec, w.dep_pix, w.seg_key, w.wcarry,
                      w.seg_start, w.seg_order, w.counters, w.counters + 1, (CinG*)w.cin,
                      w.team_blocks, w.long_len, (TeamState*)w.team, w.trace, w.coop_group,
-                     w.wave_k, w.resolve_k, w.epoch, w.helpers, w.hand_run);
+                     w.wave_k, w.resolve_k, w.epoch, w.helpers, w.hand_run, w.inject);
   if (ev) (void)hipEventRecord(ev[1], stream);
   hipLaunchKernelGGL(k_shard_cin, dim3(row_blocks), dim3(256), 0, stream, rs, o, G, rmax, H,
                      w.row_off, (const CinG*)w.cin, (CinG*)cin_ret);

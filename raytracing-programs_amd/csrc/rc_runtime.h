@@ -51,6 +51,38 @@ struct FrameBufs {
       counters, team, trace;
 };
 
+// Per-frame verification of parity frames.  A frame's carry hand-offs (the resolver team's
+// granules, phase C's carry-ins, the helper queue) are bounded spins that record the first
+// failure in the frame's TeamState (rc_kernels.hip); the next frame in the same workspace
+// resets that state.  So after every parity frame's last kernel the TeamState's first four
+// words are copied, on the frame's own stream, into a pinned ring entry the host pre-filled
+// with kPending: once the copy has run the entry holds 0 (every hand-off completed) or the
+// failure's code, workgroup and details.  The copy precedes the event that gates the
+// workspace's next use, so no later frame can erase a failure before the host has read it.
+struct FrameLog {
+  static constexpr int kRing = 4096;
+  static constexpr int kPending = 0x7fffffff;
+  struct Entry {
+    int code, block, info, info2;   // TeamState.error, err_block, err_info, err_info2
+  };
+  Entry* ring = nullptr;     // pinned host memory, kRing entries
+  long long head = 0;        // frames logged
+  long long tail = 0;        // frames whose entry has been read back (in order)
+  long long checked = 0;     // entries read back since the last take()
+  long long failed = 0;      // of them, frames whose hand-off failed
+  const char* what = "";
+  // Log the frame whose TeamState is `team` (device) on `st`, after its last kernel.
+  int enqueue(const void* team, hipStream_t st);
+  // Read back the entries whose copy has run (in order, stopping at the first still
+  // pending); reports each failure on stderr.  Returns the failures found.
+  long long poll();
+  // After the frames' streams are synchronised: every entry must have run (a pending one
+  // counts as a failure).  Returns the failures found.
+  long long drain();
+  // checked / failed since the last take(), then reset.
+  void take(long long* c, long long* f);
+};
+
 // Pipelined parity frames (rc_frame_submit).  The device's CUs are split in two partitions
 // (hipExtStreamCreateWithCUMask).  Partition A runs the carry resolvers: kLanes resolver
 // streams, each resolver grid sized to A/kLanes CUs (one workgroup per CU), so the resolvers in
@@ -89,6 +121,8 @@ struct Pipe {
   long long last = -1;               // slot of the last parity frame
   bool used[kSlots] = {};
   bool rt_on = true;                 // resolver timing events recorded (RC_PIPE_NO_RT: off)
+  int built_lanes = 0, built_slots = 0, built_res = 0;   // the tuning this pipeline was built with
+  FrameLog log;                      // every pipelined parity frame, in submission order
 };
 
 struct DevCtx {
@@ -126,6 +160,13 @@ struct DevCtx {
   uint8_t* pin_patch = nullptr;   // pinned: DEP entries' packed RGB
   size_t pin_bytes = 0;           // capacity of each pinned buffer, in entries
   int* pin_cnt = nullptr;         // pinned: counters[0..3]
+  FrameLog lone_log;   // every parity frame rendered in `fb` (rc_render, rc_render_device)
+  // `fb` is shared by every one-frame-at-a-time call on this device, and rc_render_device
+  // returns before its frame has run: the next enqueue on `fb` from another stream waits for
+  // the previous one (ws_ev, recorded after it on ws_stream).
+  hipEvent_t ws_ev = nullptr;
+  hipStream_t ws_stream = nullptr;
+  bool ws_valid = false;
   // One render at a time per device: the workspace, TeamState, events and streams above are
   // shared by every call on this device (rc_render, rc_render_device, rc_frame_submit).
   std::mutex mu;
@@ -133,8 +174,9 @@ struct DevCtx {
 
 extern DevCtx g_ctx[kMaxDevices];
 
-// process-wide schedule tuning (rc_set_tuning; defaults = the product's schedule)
-const rc_tuning& tune();
+// process-wide schedule tuning (rc_set_tuning; defaults = the product's schedule): a copy
+// taken under the tuning lock, so a render reads one consistent set of fields
+rc_tuning tune();
 int ctx_get(int device, DevCtx** out);
 int copy_to_host(DevCtx& c, uint8_t* host, const uint8_t* dev, size_t bytes, hipStream_t st);
 void prefault(uint8_t* p, size_t n);

@@ -99,16 +99,11 @@ def golden_key(scene, w, h, depth, mode):
 
 
 def p3_md5(img):
-    """md5 of the reference P3 encoding of img (written by the product P3 writer)."""
-    with tempfile.NamedTemporaryFile(suffix=".ppm", dir="/tmp") as tf:
-        write_p3(img, tf.name)
-        return file_md5(tf.name)
+    """md5 of the reference P3 encoding of img (the product P3 writer, into memory)."""
+    return rc.p3_md5(img)
 
 
-class PPMFormat(ctypes.Structure):
-    _fields_ = [("width", ctypes.c_int), ("height", ctypes.c_int), ("size", ctypes.c_int),
-                ("maxColor", ctypes.c_uint8), ("depth", ctypes.c_uint8),
-                ("tupleType", ctypes.c_char_p), ("pixmap", ctypes.c_void_p)]
+PPMFormat = rc.PPMFormat   # one ctypes class: argtypes set by either side stay compatible
 
 
 def write_p3(img, path, lib=None):

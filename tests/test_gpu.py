@@ -262,6 +262,8 @@ def test_frames_in_flight(pipe, scenes, table):
         tim = {}
         rc.frames_wait(tim)
         assert tim["resolve_ms"] > 0.0 or PIPES[pipe].get("pipe_timing") == 0
+        # every parity frame's hand-off words read back (the fast-mode frame has none)
+        assert (tim["frames_checked"], tim["frames_failed"]) == (7, 0), tim
         for key, scene, w, h, d, mode, buf in jobs:
             assert p3_md5(buf.cpu().numpy()) == table[key]["md5"], (pipe, key)
     rc.set_tuning(**saved)
@@ -360,24 +362,32 @@ def test_phantom_lit():
 
 def test_bench_sequence_8192(table):
     """bench.py's order at the C5 image size (a lone frame issued after the frame
-    pipeline once timed out): lone rc_render_device frames, then >= 20 frames in flight, then
-    lone rc_render frames into host memory — every image md5-equal to the reference's."""
+    pipeline once timed out): lone rc_render_device frames, then 22 frames in flight, then
+    lone rc_render frames into host memory — every image md5-equal to the reference's (each
+    in-flight frame has its own buffer: bytes equal to frame 0's on the device, frame 0's md5)
+    and every frame's carry hand-offs read back."""
     torch = pytest.importorskip("torch")
     n = 8192
     want = table["quadric:8192x8192:d6:parity"]["md5"]
     s = rc.Scene.from_file(scene_path("quadric"))
     out = torch.empty((n, n, 3), dtype=torch.uint8, device="cuda")
+    rc.lone_frames_check()
     for _ in range(2):
         rc.render_device(s, n, n, out.data_ptr(), depth=6, mode="parity")
     torch.cuda.synchronize()
+    assert rc.lone_frames_check() == {"checked": 2, "failed": 0}
     assert p3_md5(out.cpu().numpy()) == want, "lone device frame"
-    outs = [torch.empty((n, n, 3), dtype=torch.uint8, device="cuda") for _ in range(4)]
+    outs = [torch.empty((n, n, 3), dtype=torch.uint8, device="cuda") for _ in range(22)]
     torch.cuda.synchronize()
-    for i in range(22):
-        rc.frame_submit(s, n, n, outs[i % 4].data_ptr(), depth=6, mode="parity")
     rc.frames_wait()
     for o in outs:
-        assert p3_md5(o.cpu().numpy()) == want, "in flight"
+        rc.frame_submit(s, n, n, o.data_ptr(), depth=6, mode="parity")
+    tim = {}
+    rc.frames_wait(tim)
+    assert (tim["frames_checked"], tim["frames_failed"]) == (22, 0)
+    assert p3_md5(outs[0].cpu().numpy()) == want, "in flight, frame 0"
+    for i, o in enumerate(outs):
+        assert torch.equal(o, outs[0]), f"in flight, frame {i}"
     del outs
     for i in range(2):
         assert p3_md5(rc.render(s, n, n, depth=6, mode="parity")) == want, f"lone rc_render {i}"
@@ -522,3 +532,109 @@ def test_lone_renders_beside_frames_in_flight(scenes, table):
         assert md5 == table[key]["md5"], ("lone", key)
     for key, buf in zip(seq, bufs):
         assert p3_md5(buf.cpu().numpy()) == table[key]["md5"], ("in flight", key)
+
+
+def test_injected_hand_off_failure_in_flight(scenes, table):
+    """a failed carry hand-off in frame 2 of 8 in flight
+    (rc_debug_inject_error: its resolver raises the error word as a timed-out spin would) is
+    caught although slot 2 is reused by frame 6 (which resets the TeamState): rc_frame_submit
+    refuses new frames once the failure has arrived, rc_frames_wait raises and counts it, the
+    other frames are byte-identical, and the pipeline then renders and verifies normally."""
+    torch = pytest.importorskip("torch")
+    n, key = 1024, "quadric:1024x1024:d6:parity"
+    want = table[key]["md5"]
+    s = scenes["quadric"]
+    bufs = [torch.zeros((n, n, 3), dtype=torch.uint8, device="cuda") for _ in range(8)]
+    torch.cuda.synchronize()
+    rc.frames_wait()
+    rc.inject_error(2)
+    submitted = 0
+    try:
+        for b in bufs:
+            rc.frame_submit(s, n, n, b.data_ptr(), depth=6)
+            submitted += 1
+    except RuntimeError:
+        assert submitted > 2, "refused before the failing frame was submitted"
+    with pytest.raises(RuntimeError, match=f"1 of {submitted} frames"):
+        rc.frames_wait()
+    for i in range(submitted):
+        if i != 2:
+            assert p3_md5(bufs[i].cpu().numpy()) == want, f"frame {i}"
+    for b in bufs[:4]:
+        rc.frame_submit(s, n, n, b.data_ptr(), depth=6)
+    tim = {}
+    rc.frames_wait(tim)
+    assert (tim["frames_checked"], tim["frames_failed"]) == (4, 0)
+    for b in bufs[:4]:
+        assert p3_md5(b.cpu().numpy()) == want
+
+
+def test_injected_hand_off_failure_lone(scenes, table):
+    """One frame at a time: rc_render_device returns before its frame has run, so a failed
+    hand-off is reported by the device's next call (once), or by rc_render_device with timing
+    for its own frame, or by rc_lone_frames_check."""
+    torch = pytest.importorskip("torch")
+    n, key = 1024, "quadric:1024x1024:d6:parity"
+    want = table[key]["md5"]
+    s = scenes["quadric"]
+    out = torch.empty((n, n, 3), dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    rc.lone_frames_check()
+    rc.inject_error(0)
+    rc.render_device(s, n, n, out.data_ptr(), depth=6)   # enqueued: returns at once
+    torch.cuda.synchronize()
+    with pytest.raises(RuntimeError):
+        rc.render_device(s, n, n, out.data_ptr(), depth=6)   # reports the previous frame
+    rc.render_device(s, n, n, out.data_ptr(), depth=6)
+    torch.cuda.synchronize()
+    assert p3_md5(out.cpu().numpy()) == want
+    assert rc.lone_frames_check() == {"checked": 1, "failed": 0}
+    rc.inject_error(0)
+    with pytest.raises(RuntimeError):
+        rc.render_device(s, n, n, out.data_ptr(), depth=6, timing={})
+    rc.inject_error(0)
+    rc.render_device(s, n, n, out.data_ptr(), depth=6)
+    with pytest.raises(RuntimeError, match="1 of 1"):
+        rc.lone_frames_check()
+    tim = {}
+    rc.render_device(s, n, n, out.data_ptr(), depth=6, timing=tim)
+    assert tim["frames_checked"] == 1 and tim["frames_failed"] == 0
+    assert p3_md5(out.cpu().numpy()) == want
+    with pytest.raises(RuntimeError):   # rc_render (host pixmap) reports its own frame
+        rc.inject_error(0)
+        rc.render(s, n, n, depth=6)
+    assert p3_md5(rc.render(s, n, n, depth=6)) == want
+
+
+def test_render_device_two_streams(scenes, table):
+    """rc_render_device returns before its frame has run; a second caller on
+    another stream must not overwrite the shared one-frame workspace meanwhile (the workspace
+    event orders the two streams).  Two threads, two torch streams, md5 of every image."""
+    import threading
+    torch = pytest.importorskip("torch")
+    keys = [("quadric", 4096, 6), ("reflection", 2048, 4)]
+    res, errs = {}, []
+
+    def worker(i):
+        try:
+            name, n, d = keys[i]
+            st = torch.cuda.Stream()
+            bufs = [torch.empty((n, n, 3), dtype=torch.uint8, device="cuda") for _ in range(3)]
+            torch.cuda.synchronize()
+            for b in bufs:
+                rc.render_device(scenes[name], n, n, b.data_ptr(), st.cuda_stream, depth=d)
+            st.synchronize()
+            res[i] = [p3_md5(b.cpu().numpy()) for b in bufs]
+        except Exception as e:   # pragma: no cover - reported below
+            errs.append(repr(e))
+
+    ts = [threading.Thread(target=worker, args=(i,)) for i in range(2)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(120)
+    assert not errs, errs
+    for i, (name, n, d) in enumerate(keys):
+        want = table[f"{name}:{n}x{n}:d{d}:parity"]["md5"]
+        assert res[i] == [want] * 3, name
+    assert rc.lone_frames_check()["failed"] == 0
