@@ -29,7 +29,7 @@ HIP_SRCS  := $(SRC)/rc_kernels.hip $(SRC)/rc_api.hip $(SRC)/rc_shard.hip
 HIP_HDRS  := $(SRC)/rc_device.hpp $(SRC)/rc_cudasem.hpp $(SRC)/rc_kernels.h $(SRC)/rc_runtime.h $(SRC)/rc_scene.h include/raycast_hip.h
 FRONT_SRC := $(SRC)/front/parse.c $(SRC)/front/objects.c $(SRC)/front/ppm.c
 
-.PHONY: all oracle ref clean stamps sanitize
+.PHONY: all oracle ref clean stamps stamps2 sanitize
 all: $(LIB)/libraycast_hip.so $(LIB)/libraycast_front.so $(BIN)/raytrace oracle
 
 $(OBJ)/%.o: $(SRC)/%.hip $(HIP_HDRS)
@@ -64,6 +64,16 @@ $(OBJ)/stamps_api.o: $(SRC)/rc_api.hip $(HIP_HDRS)
 	@mkdir -p $(OBJ)
 	$(HIPCC) $(HIPFLAGS) -DRC_STAMPS=1 -DRC_DIAG=1 -c $< -o $@
 $(LIB)/libraycast_hip_stamps.so: $(OBJ)/stamps_kernels.o $(OBJ)/stamps_api.o $(OBJ)/rc_shard.o $(OBJ)/rc_scene.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -o $@ $(HIPLIBS)
+# coarse stamps: only per-step cycle counts (the evaluator itself is the product code)
+stamps2: $(LIB)/libraycast_hip_stamps2.so
+$(OBJ)/stamps2_kernels.o: $(SRC)/rc_kernels.hip $(HIP_HDRS)
+	@mkdir -p $(OBJ)
+	$(HIPCC) $(HIPFLAGS) -DRC_STAMPS=2 -DRC_DIAG=1 -c $< -o $@
+$(OBJ)/stamps2_api.o: $(SRC)/rc_api.hip $(HIP_HDRS)
+	@mkdir -p $(OBJ)
+	$(HIPCC) $(HIPFLAGS) -DRC_STAMPS=2 -DRC_DIAG=1 -c $< -o $@
+$(LIB)/libraycast_hip_stamps2.so: $(OBJ)/stamps2_kernels.o $(OBJ)/stamps2_api.o $(OBJ)/rc_shard.o $(OBJ)/rc_scene.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -o $@ $(HIPLIBS)
 
 oracle:

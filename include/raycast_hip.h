@@ -271,6 +271,8 @@ typedef struct rc_tuning {
                              beside the resolver), 0 = one per CU                            */
   int comp_stream;        /* frames in flight: compaction on an unmasked top-priority stream
                              (0 never, 1 always, 2 for images of >= 32 Mpixel)              */
+  int block_min;          /* regular carry segments of >= block_min entries are resolved by a
+                             whole resolver workgroup (block windows), 0 = never             */
 } rc_tuning;
 void rc_default_tuning(rc_tuning *t);
 int rc_set_tuning(const rc_tuning *t);

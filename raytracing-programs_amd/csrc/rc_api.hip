@@ -63,6 +63,7 @@ rc_tuning default_tuning() {
   t.copy_threads = 8;
   t.side_blocks = 0;
   t.comp_stream = 2;
+  t.block_min = 0;   // measured: 2048 slower in flight (5.46e9 vs 6.30e9) and at 8192^2
   return t;
 }
 rc_tuning g_tune = default_tuning();
@@ -369,6 +370,7 @@ int rc_set_tuning(const rc_tuning* t) {
       in(t->pipe_timing, 0, 1) && in(t->pipe_slotstreams, 0, 1) && in(t->overlap_d2h, 0, 1) &&
       in(t->staged_d2h, 0, 1) && in(t->prefault, 0, 1) && in(t->copy_threads, 1, 32) &&
       in(t->comp_stream, 0, 2) && in(t->side_blocks, 0, 1 << 16) &&
+      in(t->block_min, 0, 1 << 30) &&
       !(t->split_shade && !t->side);
   if (!ok) {
     std::fprintf(stderr, "Error: rc_set_tuning: a field is out of range\n");
@@ -609,6 +611,7 @@ int ensure_parity(DevCtx& c, FrameBufs& b, int W, int H, rc::ParityWork& w, int 
   if (w.team_blocks + w.helpers > w.resolve_blocks * 3 / 4) w.helpers = 0;
   w.hand_run = tu.hand_run;
   w.long_len = tu.long_len;
+  w.block_min = tu.block_min;
   w.wave_k = tu.wave_k;
   w.resolve_k = tu.resolve_k;
   w.coop_group = 0;
@@ -622,6 +625,7 @@ int ensure_parity(DevCtx& c, FrameBufs& b, int W, int H, rc::ParityWork& w, int 
 #if RC_DIAG   // diagnostic build (make stamps): per-segment resolver trace
   if (std::getenv("RC_RESOLVE_TRACE")) {
     if (b.trace.ensure(P * 7 * sizeof(unsigned))) return -1;
+    if (hipMemset(b.trace.p, 0, b.trace.bytes) != hipSuccess) return -1;
     w.trace = (unsigned*)b.trace.p;
   }
 #endif
@@ -804,6 +808,39 @@ void fill_device_timing(DevCtx& c, const rc_options* opt, rc_timing* t) {
         std::string p4 = std::string(path) + ".start";
         if (FILE* f = std::fopen(p4.c_str(), "w")) {
           for (int k = 0; k < cnt[0]; ++k) std::fprintf(f, "%d %u\n", k, st[k]);
+          std::fclose(f);
+        }
+      }
+      {   // when each resolver wave left (block * 4 + wave)
+        std::vector<unsigned> we(4096);
+        (void)hipMemcpy(we.data(),
+                        (const unsigned*)c.fb.trace.p + 3 * (size_t)cnt[2] + 5 * (size_t)cnt[0] +
+                            8 * 8192,
+                        we.size() * sizeof(unsigned), hipMemcpyDeviceToHost);
+        std::string p5 = std::string(path) + ".waves";
+        if (FILE* f = std::fopen(p5.c_str(), "w")) {
+          for (int k = 0; k < 4096; ++k)
+            if (we[k]) std::fprintf(f, "%d %u\n", k, we[k]);
+          std::fclose(f);
+        }
+      }
+      {   // team rounds' eval/step cycles and the helper items
+        const unsigned* b0 = (const unsigned*)c.fb.trace.p + 3 * (size_t)cnt[2] +
+                             5 * (size_t)cnt[0] + 8 * 8192 + 4096;
+        std::vector<unsigned> te(16384 + 8 * 64 + 8192);
+        (void)hipMemcpy(te.data(), b0, te.size() * sizeof(unsigned), hipMemcpyDeviceToHost);
+        std::string p6 = std::string(path) + ".cyc";
+        if (FILE* f = std::fopen(p6.c_str(), "w")) {
+          for (int r = 0; r < 8192; ++r)
+            if (te[2 * r] | te[2 * r + 1])
+              std::fprintf(f, "round %d eval %u step %u wait %u\n", r, te[2 * r], te[2 * r + 1],
+                           te[16384 + 8 * 64 + r]);
+          for (int k = 0; k < 64; ++k) {
+            const unsigned* ti = &te[16384 + 8 * k];
+            if (ti[2])
+              std::fprintf(f, "item %d seg %u wait %u t0 %u t1 %u coop %u changers %u eval %u step %u\n",
+                           k, ti[0], ti[1], ti[2], ti[3], ti[4], ti[5], ti[6], ti[7]);
+          }
           std::fclose(f);
         }
       }

@@ -929,12 +929,18 @@ __device__ __forceinline__ unsigned long long stamp_now() {
 }
 #define RC_STAMP_DECL Stamps* st_
 #define RC_STAMP_ARG , st_
+#if RC_STAMPS == 1   // per-section stamps inside the evaluator (2: coarse, per step only)
 #define RC_STAMP(i)                                  \
   do {                                               \
     const unsigned long long n_ = stamp_now();       \
     st_->acc[i] += n_ - st_->last;                   \
     st_->last = n_;                                  \
   } while (0)
+#else
+#define RC_STAMP(i) \
+  do {              \
+  } while (0)
+#endif
 #else
 #define RC_STAMP(i) \
   do {              \
@@ -1094,7 +1100,9 @@ __device__ __forceinline__ V3 carry_path_spec(const Scene& sc, const LaneShape& 
   int lvl = 2;
   while (lvl < maxrec) {
     if (!reflective(sc, obj)) break;
-    RC_STAMP(0);
+#if RC_STAMPS == 1
+    st_->last = stamp_now();   // acc[0] is the wave's LANE passes (wave_window)
+#endif
     const V3 myD = sel(half, D2, D1);
     const int myS = half ? -1 : S;
     const RayK rk = ray_consts(myD);

@@ -70,6 +70,7 @@ struct ParityWork {
   int defer_c;              // pipelined: launch_parity stops after the resolver; phase C is
                             // enqueued later by launch_phase_c (after rdone)
   int inject;               // test aid: the resolver raises its error word (code 4) at start
+  int block_min;            // regular segments of >= block_min entries get a whole workgroup
 };
 
 constexpr int kSegOrderMax = 65536;   // segments ordered for the resolver queue (else FIFO)

@@ -560,6 +560,10 @@ __device__ __forceinline__ DepRec shfl_rec(const DepRec& r, int src) {
 // evaluation steps; *changed tells whether any entry of the window moved the carry.
 struct WinStats {
   int lane, coop, changers;
+#if RC_STAMPS   // diagnostic build: cycles inside the evaluations / whole steps / waiting at
+                // the step's barrier (block_window)
+  unsigned long long ce, cs, cw;
+#endif
 };
 
 // Carry predictor for dense runs.  Inside a run of changers the carry creeps: at quadric
@@ -590,11 +594,14 @@ __device__ __forceinline__ void hist_push(CarryHist& hs, V3 c) {
 // guess q (1..) of the carry after c: the mean delta of the history, in float bits, with the
 // moving component offset by 0, -1, +1, -2, +2, ...
 __device__ __forceinline__ V3 hist_guess(const CarryHist& hs, V3 c, int q) {
-  const V3 o = hs.h[hs.n - 1];
-  const int m = hs.n - 1;
+  // no run-time index into h[] (it would put the history in scratch memory, whose reload
+  // waits for every store in flight — the carry-in publications) and no run-time divisor
+  const int m = hs.n - 1;   // 1..3
+  const V3 o = sel(m == 3, hs.h[3], sel(m == 2, hs.h[2], hs.h[1]));   // not a struct ?:
   auto md = [&](float a, float b) {
     const int d = (int)(__float_as_uint(a) - __float_as_uint(b));
-    return (d + (d >= 0 ? m / 2 : -(m / 2))) / m;
+    const int r = d >= 0 ? 1 : -1;   // m / 2 rounded away from zero, for m = 2, 3
+    return m == 1 ? d : (m == 2 ? (d + r) / 2 : (d + r) / 3);
   };
   int dx = md(hs.h[0].x, o.x), dy = md(hs.h[0].y, o.y), dz = md(hs.h[0].z, o.z);
   const int j = q - 1;
@@ -644,8 +651,14 @@ __device__ __forceinline__ int wave_window(const Scene& sc, int maxrec,
       const bool act = valid && lane >= pos;
       V3 o = c;
       bool h = false;
+#if RC_STAMPS
+      const unsigned long long tl0_ = stamp_now();
+#endif
       if (act) o = carry_path(sc, r, maxrec, c, zero, h);
       const unsigned long long m = __ballot(act && !same_bits(o, c));
+#if RC_STAMPS
+      st_->acc[0] += stamp_now() - tl0_;
+#endif
       if (m == 0) {
         if (act) {
           mine = c;
@@ -671,11 +684,14 @@ __device__ __forceinline__ int wave_window(const Scene& sc, int maxrec,
       continue;
     }
     ++ws.coop;
+#if RC_STAMPS == 2   // coarse: acc[1] = evaluations, acc[2] = whole cooperative steps
+    const unsigned long long cs0_ = __builtin_amdgcn_s_memtime();
+#endif
     // predictive step (CarryHist): group 0 takes entry pos at c, the others entry pos+1 at
     // guessed carry-ins; otherwise groups take entries pos, pos+1, .. all at c
     const bool predict = hs.n >= 2 && E >= 2 && pos + 1 < nvalid && kPredict;
     const int i = predict ? pos + (e > 0 ? 1 : 0) : pos + e;
-    const V3 ce = (predict && e > 0 && e < E) ? hist_guess(hs, c, e) : c;
+    const V3 ce = sel(predict && e > 0 && e < E, hist_guess(hs, c, e), c);
     const bool act = e < E && i < nvalid;
     const DepRec ri = shfl_rec(r, i < 64 ? i : 63);
     V3 oc = ce;
@@ -695,6 +711,14 @@ __device__ __forceinline__ int wave_window(const Scene& sc, int maxrec,
     }
 #undef RC_SPEC
 #undef RC_SPEC1
+#if RC_STAMPS == 2
+    st_->acc[1] += __builtin_amdgcn_s_memtime() - cs0_;
+    struct StepEnd_ {
+      Stamps* s;
+      unsigned long long t;
+      __device__ ~StepEnd_() { s->acc[2] += __builtin_amdgcn_s_memtime() - t; }
+    } step_end_{st_, cs0_};
+#endif
     if (predict) {
       const V3 o0 = v3(__shfl(oc.x, 0, 64), __shfl(oc.y, 0, 64), __shfl(oc.z, 0, 64));
       const bool h0 = __shfl((int)hg, 0, 64) != 0;
@@ -870,15 +894,23 @@ __device__ __forceinline__ bool cin_get(CinG* cin, int j, unsigned tag, V3& c, b
 // at once instead of after the queue reaches them.  One block: a counting sort into 256
 // length buckets of 32 entries (>= 8160 share the top bucket), stable within a bucket.
 // Above kSegOrderMax segments the queue stays in segment order (counters[3] = 0).
+// The order's first counters[14] segments have >= block_min entries (rounded up to the
+// bucket width): k_resolve's workgroups take them from head A (counters[1]) while its waves
+// start on the rest from head B (counters[15]).
 __global__ void __launch_bounds__(1024) k_seg_order(const int* __restrict__ seg_start,
                                                      int* __restrict__ counters,
                                                      int* __restrict__ order,
-                                                     int* __restrict__ batch_state) {
+                                                     int* __restrict__ batch_state,
+                                                     int block_min) {
   const int nseg = counters[0], ndep = counters[2];
   // phase C's per-batch claim words (64 DEP entries per batch), zeroed for this frame
   for (int b = threadIdx.x; b < (ndep + 63) / 64; b += blockDim.x) batch_state[b] = 0;
   if (nseg > kSegOrderMax) {
-    if (threadIdx.x == 0) counters[3] = 0;
+    if (threadIdx.x == 0) {
+      counters[3] = 0;
+      counters[14] = 0;
+      counters[15] = 0;
+    }
     return;
   }
   __shared__ int hist[256];
@@ -897,11 +929,16 @@ __global__ void __launch_bounds__(1024) k_seg_order(const int* __restrict__ seg_
   for (int s = s0; s < s1; ++s) atomicAdd(&hist[bucket(s)], 1);
   __syncthreads();
   if (t == 0) {
-    int acc = 0;
+    int acc = 0, nlong = 0;
+    int bmin = (block_min + 31) >> 5;   // smallest length bucket taken by workgroups
+    if (bmin > 255) bmin = 255;
     for (int b = 0; b < 256; ++b) {
       off[b] = acc;
       acc += hist[b];
+      if (block_min > 0 && 255 - b >= bmin) nlong = acc;
     }
+    counters[14] = nlong;
+    counters[15] = nlong;
   }
   __syncthreads();
   for (int s = s0; s < s1; ++s) order[atomicAdd(&off[bucket(s)], 1)] = s;
@@ -920,11 +957,11 @@ struct BlockWinShared {
   uint8_t hit[kResolveBlock];   // per entry: some level hit at the window's carry
   int wpos[2][4];
   float wout[2][4][3];
-  // predictive steps (helper blocks): per group its output, hit flag and guess
-  float pout[16][3];
-  float pce[16][3];
-  int phit[16];
-  int pmatch;
+  // predictive steps (helper blocks): per group its output, hit flag and guess, double-
+  // buffered by step parity like wpos / wout (one barrier per step)
+  float pout[2][16][3];
+  float pce[2][16][3];
+  int phit[2][16];
 };
 
 // hp (helper blocks): carry predictor; the cooperative step then takes entry pos at c in
@@ -948,7 +985,17 @@ __device__ __forceinline__ void block_window(const Scene& sc, int maxrec, BlockW
   const int E = 64 / GE;
   const int Eb = 4 * E;
   const int e = lane / GE, kself = G > 0 ? lane % G : 0, half = spec ? (lane / G) & 1 : 0;
+#if RC_STAMPS
+  unsigned long long top_ = 0;
+#endif
   while (pos < nvalid) {
+#if RC_STAMPS
+    {
+      const unsigned long long n_ = __builtin_amdgcn_s_memtime();
+      if (top_) ws.cs += n_ - top_;
+      top_ = n_;
+    }
+#endif
     int last;      // entries [pos, last] resolve with carry c
     V3 cn = c;
     bool hit;
@@ -956,7 +1003,7 @@ __device__ __forceinline__ void block_window(const Scene& sc, int maxrec, BlockW
       ++ws.coop;
       const int gi = wave * E + e;
       const int i = pos + (gi > 0 ? 1 : 0);
-      const V3 ce = gi > 0 ? hist_guess(*hp, c, gi) : c;
+      const V3 ce = sel(gi > 0, hist_guess(*hp, c, gi), c);
       const DepRec ri = bw.rec[i];
       V3 oc = ce;
       bool hg = false;
@@ -973,26 +1020,36 @@ __device__ __forceinline__ void block_window(const Scene& sc, int maxrec, BlockW
       else oc = RC_SPEC(0);
 #undef RC_SPEC
 #undef RC_SPEC1
+#if RC_STAMPS
+      ws.ce += __builtin_amdgcn_s_memtime() - top_;
+#endif
       if ((lane % GE) == 0) {
-        bw.pout[gi][0] = oc.x;
-        bw.pout[gi][1] = oc.y;
-        bw.pout[gi][2] = oc.z;
-        bw.pce[gi][0] = ce.x;
-        bw.pce[gi][1] = ce.y;
-        bw.pce[gi][2] = ce.z;
-        bw.phit[gi] = hg ? 1 : 0;
+        bw.pout[par][gi][0] = oc.x;
+        bw.pout[par][gi][1] = oc.y;
+        bw.pout[par][gi][2] = oc.z;
+        bw.pce[par][gi][0] = ce.x;
+        bw.pce[par][gi][1] = ce.y;
+        bw.pce[par][gi][2] = ce.z;
+        bw.phit[par][gi] = hg ? 1 : 0;
       }
+      // one barrier per step: every wave finds the matching guess itself (the same ballot
+      // over the same slots), and the slots are double-buffered by step parity — a wave
+      // writes parity p again only after every wave has passed the barrier of the step
+      // in between, i.e. has read these
+#if RC_STAMPS
+      const unsigned long long bw0_ = __builtin_amdgcn_s_memtime();
+#endif
       __syncthreads();
-      const V3 o0 = v3(bw.pout[0][0], bw.pout[0][1], bw.pout[0][2]);
-      if (wave == 0) {
-        const bool mt = lane > 0 && lane < Eb &&
-                        same_bits(v3(bw.pce[lane][0], bw.pce[lane][1], bw.pce[lane][2]), o0);
-        const unsigned long long mm = __ballot(mt);
-        if (lane == 0) bw.pmatch = mm ? __ffsll((long long)mm) - 1 : 0;
-      }
-      __syncthreads();
-      const int mi = bw.pmatch;
-      if (t == pos) cin_put(cin, base + pos, c, tag, bw.phit[0] != 0);
+#if RC_STAMPS
+      ws.cw += __builtin_amdgcn_s_memtime() - bw0_;
+#endif
+      const V3 o0 = v3(bw.pout[par][0][0], bw.pout[par][0][1], bw.pout[par][0][2]);
+      const bool mt = lane > 0 && lane < Eb &&
+                      same_bits(v3(bw.pce[par][lane][0], bw.pce[par][lane][1],
+                                   bw.pce[par][lane][2]), o0);
+      const unsigned long long mm = __ballot(mt);
+      const int mi = mm ? __ffsll((long long)mm) - 1 : 0;
+      if (t == pos) cin_put(cin, base + pos, c, tag, bw.phit[par][0] != 0);
       if (same_bits(o0, c)) {   // entry pos leaves the carry: the run is over
         hp->n = 0;
         pos += 1;
@@ -1003,8 +1060,8 @@ __device__ __forceinline__ void block_window(const Scene& sc, int maxrec, BlockW
         clean_run = 0;
         hist_push(*hp, o0);
         if (mi > 0) {
-          const V3 o1 = v3(bw.pout[mi][0], bw.pout[mi][1], bw.pout[mi][2]);
-          if (t == pos + 1) cin_put(cin, base + pos + 1, o0, tag, bw.phit[mi] != 0);
+          const V3 o1 = v3(bw.pout[par][mi][0], bw.pout[par][mi][1], bw.pout[par][mi][2]);
+          if (t == pos + 1) cin_put(cin, base + pos + 1, o0, tag, bw.phit[par][mi] != 0);
           pos += 2;
           if (same_bits(o1, o0)) {
             hp->n = 0;
@@ -1019,7 +1076,7 @@ __device__ __forceinline__ void block_window(const Scene& sc, int maxrec, BlockW
           pos += 1;
         }
       }
-      __syncthreads();   // pout / pmatch are rewritten by the next step
+      par ^= 1;
       continue;
     }
     if (!coop) {
@@ -1028,6 +1085,9 @@ __device__ __forceinline__ void block_window(const Scene& sc, int maxrec, BlockW
       V3 o = c;
       bool h = false;
       if (act) o = carry_path(sc, bw.rec[t], maxrec, c, zero, h);
+#if RC_STAMPS
+      ws.ce += __builtin_amdgcn_s_memtime() - top_;
+#endif
       bw.hit[t] = h ? 1 : 0;
       const unsigned long long m = __ballot(act && !same_bits(o, c));
       const int k = m ? __ffsll((long long)m) - 1 : -1;
@@ -1060,6 +1120,9 @@ __device__ __forceinline__ void block_window(const Scene& sc, int maxrec, BlockW
       }
 #undef RC_SPEC
 #undef RC_SPEC1
+#if RC_STAMPS
+      ws.ce += __builtin_amdgcn_s_memtime() - top_;
+#endif
       if (act && (lane % GE) == 0) bw.hit[i] = hg ? 1 : 0;
       const unsigned long long mc = __ballot(act && (lane % GE) == 0 && !same_bits(oc, c));
       const int g = mc ? (__ffsll((long long)mc) - 1) / GE : -1;
@@ -1070,7 +1133,13 @@ __device__ __forceinline__ void block_window(const Scene& sc, int maxrec, BlockW
         bw.wout[par][wave][2] = oc.z;
       }
     }
+#if RC_STAMPS
+    const unsigned long long bw1_ = __builtin_amdgcn_s_memtime();
+#endif
     __syncthreads();
+#if RC_STAMPS
+    ws.cw += __builtin_amdgcn_s_memtime() - bw1_;
+#endif
     int wb = 0;
     int best = bw.wpos[par][0];
     for (int q = 1; q < 4; ++q) {
@@ -1113,6 +1182,9 @@ __device__ __forceinline__ void block_window(const Scene& sc, int maxrec, BlockW
       if (++clean_run >= K) coop = false;
     }
   }
+#if RC_STAMPS
+  if (top_) ws.cs += __builtin_amdgcn_s_memtime() - top_;
+#endif
   dense = coop;
 }
 
@@ -1225,7 +1297,7 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
     int* __restrict__ counters, int* __restrict__ head,
     CinG* __restrict__ cin, int team_blocks, int long_len, TeamState* __restrict__ ts,
     unsigned* __restrict__ trace, int G, int wave_k, int resolve_k, unsigned tag,
-    int helpers, int hand_run, int inject) {
+    int helpers, int hand_run, int inject, int block_min) {
   // census for phase C's side kernel: it only proceeds once every resolver block is resident
   if (threadIdx.x == 0)
     __hip_atomic_fetch_add(&counters[5], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1279,10 +1351,19 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
     const int T = team_blocks;
     const int window = T * 4 * 64;
     int round = 0;
-    for (int s = 0; s < nseg; ++s) {
+    // the long segments lead the length-ordered queue (k_seg_order): stop at the first
+    // shorter one instead of walking the whole segment table with dependent loads (0.4 ms at
+    // quadric 4096^2, 2 076 segments, after the team's one segment was done)
+    for (int q = 0; q < nseg; ++q) {
+      const int s = ordered ? seg_order[q] : q;
       const int start = seg_start[s];
       const int end = (s + 1 < nseg) ? seg_start[s + 1] : ndep;
-      if (end - start < long_len) continue;
+      if (end - start < long_len) {
+        // below the floor of long_len's length bucket (k_seg_order: 32-entry buckets, the
+        // top one holds every length >= 8160 unsorted): no long segment follows
+        if (ordered && (end - start) < (min(long_len >> 5, 255) << 5)) break;
+        continue;
+      }
       const unsigned long long t_seg = __builtin_amdgcn_s_memrealtime();
       const unsigned long long c_seg = __builtin_amdgcn_s_memtime();
       int rounds_here = 0;
@@ -1415,12 +1496,19 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
           tl[5] = (unsigned)tws.coop;
           tl[6] = (unsigned)tws.changers;
           tl[7] = 0xA5A5A5A5u;
+#if RC_STAMPS   // eval / step cycles of the round's block windows
+          unsigned* te = trace + 3 * (size_t)ndep + 5 * (size_t)nseg + 8 * 8192 + 4096;
+          te[2 * round] = (unsigned)tws.ce;
+          te[2 * round + 1] = (unsigned)tws.cs;
+          te[16384 + 8 * 64 + round] = (unsigned)tws.cw;
+#endif
         }
       }
       if (trace && blockIdx.x == 0 && threadIdx.x == 0) {
         trace[3 * s] = (unsigned)(__builtin_amdgcn_s_memrealtime() - t_seg);
         trace[3 * s + 1] = (unsigned)rounds_here | 0x80000000u;
         trace[3 * s + 2] = (unsigned)(__builtin_amdgcn_s_memtime() - c_seg);
+        trace[3 * (size_t)ndep + 4 * (size_t)nseg + 8 * 8192 + s] = (unsigned)t_seg;
       }
     }
     // the team's segments are done: its waves join the regular queue (every wave from here
@@ -1484,6 +1572,8 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
       const int end = (sg + 1 < nseg) ? seg_start[sg + 1] : ndep;
       bool dense = true;
       WinStats hws = {0, 0, 0};
+      const int j_item = j;
+      const unsigned long long t_item = __builtin_amdgcn_s_memrealtime();
       if (j + t < end) s_bw.rec[t] = rec_at(deprec, dep_pix, j + t);
       __syncthreads();
       while (j < end) {
@@ -1499,14 +1589,99 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
         if (j + t < end) s_bw.rec[t] = nxt;
         __syncthreads();
       }
+      if (trace && t == 0 && k < 64) {   // debug trace: the helper's items
+        unsigned* ti = trace + 3 * (size_t)ndep + 5 * (size_t)nseg + 8 * 8192 + 4096 + 16384 + 8 * k;
+        ti[0] = (unsigned)sg;
+        ti[1] = (unsigned)(end - j_item);
+        ti[2] = (unsigned)t_item;
+        ti[3] = (unsigned)__builtin_amdgcn_s_memrealtime();
+        ti[4] = (unsigned)hws.coop;
+        ti[5] = (unsigned)hws.changers;
+#if RC_STAMPS
+        ti[6] = (unsigned)hws.ce;
+        ti[7] = (unsigned)hws.cs;
+        ti[1] = (unsigned)hws.cw;   // (the item's length is in the segment table)
+#endif
+      }
     }
+    if (trace && lane == 0)   // debug trace: when each wave leaves
+      trace[3 * (size_t)ndep + 5 * (size_t)nseg + 8 * 8192 + blockIdx.x * 4 + wave] =
+          (unsigned)__builtin_amdgcn_s_memrealtime();
     return;   // helpers take no regular segments
+  }
+
+  // ------------------------------------------------------- long regular segments --
+  // Segments of >= block_min entries (the queue is longest first) are resolved by a whole
+  // workgroup: block_window's cooperative steps take 4*E entries (16 at G = 8) where one wave
+  // takes E, so a changer costs about one evaluation where a lone wave spends LANE passes
+  // (~26k cycles each) looking for the next one.  Lone quadric 4096^2: the 3856-entry segments
+  // took 4.3 ms on one wave (157 LANE passes and 505 cooperative steps for 377 changers).
+  // Once the queue reaches a shorter segment, the block's wave 0 takes that one and every
+  // wave goes on as a regular wave.
+  // The queue's first nlong segments (k_seg_order) are taken from head A by workgroups; the
+  // waves start at once on the rest (head B), so shorter segments that turn out dense are not
+  // held back behind the long ones, and take what is left of head A at the end.
+  const int nlong = counters[14];
+  int* headb = counters + 15;
+  if (nlong > 0 && (int)blockIdx.x >= team_blocks + helpers) {
+    __shared__ int s_seg;
+    const int t = threadIdx.x;
+    for (;;) {
+      if (t == 0) s_seg = atomicAdd(head, 1);
+      __syncthreads();
+      const int q = s_seg;
+      __syncthreads();   // s_seg is rewritten by the next dequeue
+      if (q >= nlong) break;
+      const int sg = ordered ? seg_order[q] : q;
+      const int start = seg_start[sg];
+      const int end = (sg + 1 < nseg) ? seg_start[sg + 1] : ndep;
+      if (team_blocks > 0 && end - start >= long_len) continue;   // the team's
+      const unsigned long long t_seg = __builtin_amdgcn_s_memrealtime();
+      const unsigned long long c_seg = __builtin_amdgcn_s_memtime();
+      V3 c = seg_init_carry(seg_key, wcarry, sg);
+      bool dense = false;
+      WinStats bws = {0, 0, 0};
+      int j = start;
+      if (j + t < end) s_bw.rec[t] = rec_at(deprec, dep_pix, j + t);
+      __syncthreads();
+      while (j < end) {
+        const int nv = end - j < kResolveBlock ? end - j : kResolveBlock;
+        DepRec nxt;
+        const int jn = j + nv;
+        if (jn + t < end) nxt = rec_at(deprec, dep_pix, jn + t);
+        bool changed;
+        // no carry predictor here: its steps take two entries, and a clean entry after a
+        // change ends the cooperative mode (measured: 191 LANE passes on a 3856-entry segment)
+        block_window(sc, maxrec, s_bw, j, nv, c, ls, G, dense, changed, wave_k, cin, tag,
+                     bws, nullptr);
+        j = jn;
+        __syncthreads();   // everyone is done reading this window's records
+        if (j + t < end) s_bw.rec[t] = nxt;
+        __syncthreads();
+      }
+      if (trace && t == 0) {
+        trace[3 * sg] = (unsigned)(__builtin_amdgcn_s_memrealtime() - t_seg);
+#if RC_STAMPS   // LANE passes << 16 | cooperative steps (block windows)
+        trace[3 * sg + 1] = ((unsigned)bws.lane << 16) | ((unsigned)bws.coop & 0xffffu);
+#else
+        trace[3 * sg + 1] = (unsigned)(bws.lane + bws.coop);
+#endif
+        trace[3 * sg + 2] = (unsigned)(__builtin_amdgcn_s_memtime() - c_seg);
+        trace[3 * (size_t)ndep + 4 * (size_t)nseg + 8 * 8192 + sg] = (unsigned)t_seg;
+      }
+    }
   }
 
   // ------------------------------------------------------------- regular waves --
   for (;;) {
     int s = 0;
-    if (lane == 0) s = atomicAdd(head, 1);
+    if (lane == 0) {
+      s = atomicAdd(headb, 1);
+      if (s >= nseg) {   // head B is done: any long segment no workgroup has taken yet
+        s = atomicAdd(head, 1);
+        if (s >= nlong) s = nseg;
+      }
+    }
     s = __shfl(s, 0, 64);
     if (s >= nseg) break;
     if (ordered) s = seg_order[s];
@@ -1579,7 +1754,12 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
 #endif
     if (trace && lane == 0) {
       trace[3 * s] = (unsigned)(__builtin_amdgcn_s_memrealtime() - t_seg);
+#if RC_STAMPS   // the diagnostic build splits the steps: LANE passes << 16 | COOP steps
+      trace[3 * s + 1] = ((unsigned)ws.lane << 16) | ((unsigned)ws.coop & 0xffffu);
+      (void)iters;
+#else
       trace[3 * s + 1] = (unsigned)iters;
+#endif
       trace[3 * s + 2] = (unsigned)(__builtin_amdgcn_s_memtime() - c_seg);
       // start time (low 32 bits of the 100 MHz clock) after the team log
       trace[3 * (size_t)ndep + 4 * (size_t)nseg + 8 * 8192 + s] = (unsigned)t_seg;
@@ -1588,6 +1768,9 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
   // this wave hands nothing off any more (helper blocks wait for every such wave)
   if (lane == 0)
     __hip_atomic_fetch_add(&ts->dq.finished, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  if (trace && lane == 0)   // debug trace: when each wave leaves
+    trace[3 * (size_t)ndep + 5 * (size_t)nseg + 8 * 8192 + blockIdx.x * 4 + wave] =
+        (unsigned)__builtin_amdgcn_s_memrealtime();
 }
 
 // ------------------------------------------------------------------ parity phase C --
@@ -2170,7 +2353,7 @@ hipError_t launch_parity(const LaunchScene& s, int W, int H, int maxrec, uint8_t
                      w.row_off, w.row_soff, w.row_prevw, w.row_prevd, w.dep_pix, w.seg_start,
                      w.seg_key);
   hipLaunchKernelGGL(k_seg_order, dim3(1), dim3(1024), 0, stream, w.seg_start, w.counters,
-                     w.seg_order, w.batch_state);
+                     w.seg_order, w.batch_state, w.block_min);
   // resolve_lds > 80 KiB keeps one resolver block (4 waves, one per SIMD) per CU: the chain
   // steps are latency-bound, so a resolver wave should not share its SIMD
   if (ev) (void)hipEventRecord(ev[1], stream);
@@ -2187,7 +2370,7 @@ hipError_t launch_parity(const LaunchScene& s, int W, int H, int maxrec, uint8_t
                      maxrec, (const DepRec*)w.deprec, w.dep_pix, w.seg_key, w.wcarry,
                      w.seg_start, w.seg_order, w.counters, w.counters + 1, (CinG*)w.cin, w.team_blocks,
                      w.long_len, (TeamState*)w.team, w.trace, w.coop_group, w.wave_k,
-                     w.resolve_k, w.epoch, w.helpers, w.hand_run, w.inject);
+                     w.resolve_k, w.epoch, w.helpers, w.hand_run, w.inject, w.block_min);
   if (w.rstream) {
     if (w.rt1) (void)hipEventRecord(w.rt1, rs);
     (void)hipEventRecord(w.rdone, rs);
@@ -2349,14 +2532,14 @@ hipError_t launch_shard_resolve(const LaunchScene& s, int W, int H, int G, int r
                      w.row_prevw, w.row_prevd, (DepRec*)w.deprec, w.dep_pix, w.seg_start,
                      w.seg_key, w.wcarry);
   hipLaunchKernelGGL(k_seg_order, dim3(1), dim3(1024), 0, stream, w.seg_start, w.counters,
-                     w.seg_order, w.batch_state);
+                     w.seg_order, w.batch_state, w.block_min);
   if (ev) (void)hipEventRecord(ev[0], stream);
   auto kres = s.n <= kLdsShapes ? k_resolve<true> : k_resolve<false>;
   hipLaunchKernelGGL(kres, dim3(w.resolve_blocks), dim3(kResolveBlock), w.resolve_lds, stream,
                      sc, maxrec, (const DepRec*)w.deprec, w.dep_pix, w.seg_key, w.wcarry,
                      w.seg_start, w.seg_order, w.counters, w.counters + 1, (CinG*)w.cin,
                      w.team_blocks, w.long_len, (TeamState*)w.team, w.trace, w.coop_group,
-                     w.wave_k, w.resolve_k, w.epoch, w.helpers, w.hand_run, w.inject);
+                     w.wave_k, w.resolve_k, w.epoch, w.helpers, w.hand_run, w.inject, w.block_min);
   if (ev) (void)hipEventRecord(ev[1], stream);
   hipLaunchKernelGGL(k_shard_cin, dim3(row_blocks), dim3(256), 0, stream, rs, o, G, rmax, H,
                      w.row_off, (const CinG*)w.cin, (CinG*)cin_ret);

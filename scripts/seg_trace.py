@@ -33,3 +33,16 @@ for e in ends[:15]:
 busy = sum(d["dur"] for k, d in seg.items() if k not in team) / 100.0
 print(f"regular wave-time: {busy/1000:.1f} wave-ms; longest 10 durations (us):",
       sorted((d["dur"] / 100 for k, d in seg.items() if k not in team), reverse=True)[:10])
+
+import os
+if os.path.exists(path + ".waves"):
+    we = {}
+    for l in open(path + ".waves"):
+        k, t = map(int, l.split())
+        we[k] = ((t - base) & 0xffffffff) / 100.0
+    last = sorted(we.items(), key=lambda kv: -kv[1])[:12]
+    print("last waves to leave (block*4+wave: us):", ", ".join(f"{k}: {v:.0f}" for k, v in last))
+for k in team:
+    d = seg[k]
+    if d.get("t0"):
+        print(f"team seg {k} starts at {((d['t0'] - base) & 0xffffffff) / 100:.1f} us")
