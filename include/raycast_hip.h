@@ -329,6 +329,11 @@ typedef struct rc_shard_stats {   /* the last rc_render_sharded, on the root */
   int64_t image_bytes;    /* row blocks moved to the root (padded to ceil(H/G) rows)        */
 } rc_shard_stats;
 int rc_group_last_stats(const rc_group *group, rc_shard_stats *out);
+/* Parity frames exchange the DEP entries in fixed-size per-rank blocks (no host
+ * synchronisation inside the frame) once a frame of the same scene and size has given the
+ * per-rank count; a frame that exceeds it is rendered again with exact sizes.  Test aid: set
+ * that bound (entries per rank; -1 forgets it). */
+int rc_group_debug_bound(rc_group *group, long long per_rank);
 
 /* Library version / build string. */
 const char *rc_version(void);

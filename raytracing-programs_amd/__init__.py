@@ -114,7 +114,7 @@ HIP_EXPORTS = ["raycast", "rc_default_options", "rc_scene_create", "rc_scene_des
                "rc_group_create_local", "rc_group_destroy", "rc_group_size",
                "rc_group_transport", "rc_render_sharded", "rc_group_last_stats",
                "rc_default_tuning", "rc_set_tuning", "rc_get_tuning", "rc_lone_frames_check",
-               "rc_debug_inject_error"]
+               "rc_debug_inject_error", "rc_group_debug_bound"]
 FRONT_EXPORTS = ["add_new_sphere", "add_new_plane", "add_new_quadric", "free_shape_list",
                  "free_light_list", "add_new_spot_light", "add_new_point_light", "parse_json",
                  "set_to_black", "ppm_WriteOutP3", "ppm_clamp"]
@@ -217,6 +217,7 @@ def _hip_lib_locked():
                                       ctypes.POINTER(RcOptions), ctypes.c_void_p,
                                       ctypes.POINTER(RcTiming)]
     lib.rc_group_last_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(RcShardStats)]
+    lib.rc_group_debug_bound.argtypes = [ctypes.c_void_p, ctypes.c_longlong]
     lib.rc_default_tuning.argtypes = [ctypes.POINTER(RcTuning)]
     lib.rc_default_tuning.restype = None
     lib.rc_get_tuning.argtypes = [ctypes.POINTER(RcTuning)]
@@ -571,6 +572,11 @@ class Group:
         if hip_lib().rc_group_last_stats(self._h, ctypes.byref(st)) != 0:
             raise RuntimeError("rc_group_last_stats failed")
         return {k: getattr(st, k) for k, _ in RcShardStats._fields_}
+
+    def debug_bound(self, per_rank):
+        """Test aid (rc_group_debug_bound): the fixed-size entry exchange's per-rank bound."""
+        if hip_lib().rc_group_debug_bound(self._h, int(per_rank)) != 0:
+            raise ValueError(per_rank)
 
     def close(self):
         if self._h:

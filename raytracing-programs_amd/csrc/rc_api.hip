@@ -493,7 +493,7 @@ int ensure_parity(DevCtx& c, FrameBufs& b, int W, int H, rc::ParityWork& w, int 
       b.dep_pix.ensure(P * sizeof(long long)) || b.seg_key.ensure(P * sizeof(long long)) ||
       b.seg_start.ensure(P * sizeof(int)) ||
       b.seg_order.ensure((size_t)rc::kSegOrderMax * sizeof(int)) ||
-      b.batch_state.ensure((P / 64 + 2) * sizeof(int)) ||
+      b.batch_state.ensure(3 * (P / 64 + 2) * sizeof(int)) ||
       b.counters.ensure(64) || b.team.ensure(rc::team_state_bytes()))
     return -1;
   if (P >= (size_t)1 << 31) return -1;   // DEP indices are 32-bit
@@ -541,7 +541,9 @@ int ensure_parity(DevCtx& c, FrameBufs& b, int W, int H, rc::ParityWork& w, int 
   w.seg_start = (int*)b.seg_start.p;
   w.seg_order = (int*)b.seg_order.p;
   w.cin = b.cin.p;
-  w.batch_state = (int*)b.batch_state.p;
+  w.batch_state = (int*)b.batch_state.p;   // claim words, then completion counts, then queue
+  w.batch_cnt = w.batch_state + (P / 64 + 2);
+  w.batch_rq = w.batch_state + 2 * (P / 64 + 2);
   w.side = nullptr;
   w.rstream = nullptr;
   w.pstream = nullptr;
@@ -821,6 +823,20 @@ void fill_device_timing(DevCtx& c, const rc_options* opt, rc_timing* t) {
         if (FILE* f = std::fopen(p5.c_str(), "w")) {
           for (int k = 0; k < 4096; ++k)
             if (we[k]) std::fprintf(f, "%d %u\n", k, we[k]);
+          std::fclose(f);
+        }
+      }
+      {   // k_side's ready-queue items: pop time, carries ready, batch shaded
+        const int nb = (cnt[2] + 63) / 64;
+        std::vector<unsigned> tq(3 * (size_t)nb);
+        (void)hipMemcpy(tq.data(),
+                        (const unsigned*)c.fb.trace.p + 3 * (size_t)cnt[2] + 5 * (size_t)cnt[0] +
+                            200000,
+                        tq.size() * sizeof(unsigned), hipMemcpyDeviceToHost);
+        std::string p7 = std::string(path) + ".side";
+        if (FILE* f = std::fopen(p7.c_str(), "w")) {
+          for (int k = 0; k < nb; ++k)
+            if (tq[3 * k]) std::fprintf(f, "%d %u %u %u\n", k, tq[3 * k], tq[3 * k + 1], tq[3 * k + 2]);
           std::fclose(f);
         }
       }

@@ -93,12 +93,19 @@ __device__ __forceinline__ double sqrt_ns(double s) {
   return (s == 0.0 || s == __builtin_inf()) ? s : g;
 }
 
+// ((x^2 + y^2) + z^2) in double for floats x, y, z, each addition rounded once: the square of
+// a float is exact in double (48 significant bits), so fma(y, y, x*x) rounds exactly the sum
+// the reference rounds — one instruction per term instead of a multiply and an add.
+__device__ __forceinline__ double sumsq3(double x, double y, double z) {
+  return __builtin_fma(z, z, __builtin_fma(y, y, x * x));
+}
+
+// Discriminants b*b - p with b a float and p an exact double product (4*a*c of floats, or a
+// float widened): b*b is exact too, so fma(b, b, -p) rounds the same difference once.
+
 // C/v3math.c:169-172 — (float)sqrt of an exact double sum of squares
 __device__ __forceinline__ float length(V3 a) {
-  double s = (double)a.x * (double)a.x;
-  s = s + (double)a.y * (double)a.y;
-  s = s + (double)a.z * (double)a.z;
-  return (float)sqrt_ns(s);
+  return (float)sqrt_ns(sumsq3((double)a.x, (double)a.y, (double)a.z));
 }
 
 // a_i / len for the three components through one f64 reciprocal: r = 1/len to within
@@ -209,10 +216,7 @@ struct RayK {
   double den;   // 2.0 * (double)a     (C/raycast.c:593)
 };
 __device__ __forceinline__ RayK ray_consts(V3 D) {
-  double aa = (double)D.x * (double)D.x;
-  aa = aa + (double)D.y * (double)D.y;
-  aa = aa + (double)D.z * (double)D.z;
-  float a = (float)aa;
+  float a = (float)sumsq3((double)D.x, (double)D.y, (double)D.z);
   return RayK{4.0f * a, 2.0 * (double)a};
 }
 
@@ -222,7 +226,7 @@ __device__ __forceinline__ bool hit_sphere(V3 O, V3 D, const rc_shape& s, RayK k
   float b = 2.0f * dot(D, tv);
   float c = (float)((double)dot(tv, tv) - s.r2);
   float fac = k.a4 * c;
-  float disc = (float)((double)b * (double)b - (double)fac);
+  float disc = (float)__builtin_fma((double)b, (double)b, -(double)fac);
   if (disc < 0.0f) return false;
   double sq = sqrt_ns((double)disc);
   float tt = (float)(((double)(-b) - sq) / k.den);
@@ -281,7 +285,7 @@ __device__ __forceinline__ bool hit_quadric(V3 O, V3 D, const rc_shape& q, float
     t = (float)((-1.0 * (double)cq) / (double)bq);
     return true;
   }
-  const float disc = (float)((double)bq * (double)bq - 4.0 * (double)aq * (double)cq);
+  const float disc = (float)__builtin_fma((double)bq, (double)bq, -(4.0 * (double)aq * (double)cq));
   if ((double)disc < 0.0) return false;
   const double den = 2.0 * (double)aq;
   const double sq = sqrt_ns((double)disc);
@@ -337,7 +341,7 @@ __device__ __forceinline__ bool hit_sphere_o0(V3 D, const rc_shape& s, RayK k, f
   const V3 tv = v3(0.0f - s.p[0], 0.0f - s.p[1], 0.0f - s.p[2]);
   float b = 2.0f * dot(D, tv);
   float fac = k.a4 * s.o0;
-  float disc = (float)((double)b * (double)b - (double)fac);
+  float disc = (float)__builtin_fma((double)b, (double)b, -(double)fac);
   if (disc < 0.0f) return false;
   double sq = sqrt_ns((double)disc);
   float tt = (float)(((double)(-b) - sq) / k.den);
@@ -373,7 +377,7 @@ __device__ __forceinline__ bool hit_quadric_o0(V3 D, const rc_shape& q, float& t
     t = (float)((-1.0 * (double)cq) / (double)bq);
     return true;
   }
-  const float disc = (float)((double)bq * (double)bq - 4.0 * (double)aq * (double)cq);
+  const float disc = (float)__builtin_fma((double)bq, (double)bq, -(4.0 * (double)aq * (double)cq));
   if ((double)disc < 0.0) return false;
   const double den = 2.0 * (double)aq;
   const double sq = sqrt_ns((double)disc);
@@ -433,7 +437,7 @@ __device__ __forceinline__ bool shadow_sphere(V3 O, V3 D, const rc_shape& s, Ray
   float b = 2.0f * dot(D, tv);
   float c = (float)((double)dot(tv, tv) - s.r2);
   float fac = k.a4 * c;
-  float disc = (float)((double)b * (double)b - (double)fac);
+  float disc = (float)__builtin_fma((double)b, (double)b, -(double)fac);
   if (disc < 0.0f) return false;
   double sq = sqrt_ns((double)disc);
   int q = quot_class((double)(-b) - sq, k.den);
@@ -484,7 +488,7 @@ __device__ __forceinline__ bool shadow_quadric(V3 O, V3 D, const rc_shape& q, in
     den = (double)bq;
     cls = quot_class(num, den);
   } else {
-    const float disc = (float)((double)bq * (double)bq - 4.0 * (double)aq * (double)cq);
+    const float disc = (float)__builtin_fma((double)bq, (double)bq, -(4.0 * (double)aq * (double)cq));
     if ((double)disc < 0.0) return false;
     den = 2.0 * (double)aq;
     const double sq = sqrt_ns((double)disc);
@@ -972,7 +976,7 @@ __device__ __forceinline__ bool test_unified(const rc_shape& s, V3 O, V3 D, RayK
   // direction parts (sphere b and disc, plane den)
   const float bS = 2.0f * dot(D, tv);
   const float facS = rk.a4 * cS;
-  const float discS = (float)((double)bS * (double)bS - (double)facS);
+  const float discS = (float)__builtin_fma((double)bS, (double)bS, -(double)facS);
   const float denP = dot(D, v3(s.n[0], s.n[1], s.n[2]));
   float cq = 0.0f, aq = 0.0f, bq = 0.0f, discQ = 0.0f;
   bool lin = false;
@@ -1006,7 +1010,7 @@ __device__ __forceinline__ bool test_unified(const rc_shape& s, V3 O, V3 D, RayK
     acc = acc + (double)(s.qh * D.y);
     acc = acc + (double)(s.qi * D.z);
     bq = (float)acc;
-    discQ = (float)((double)bq * (double)bq - 4.0 * (double)aq * (double)cq);
+    discQ = (float)__builtin_fma((double)bq, (double)bq, -(4.0 * (double)aq * (double)cq));
     lin = (double)aq == 0.0;
   }
   // shared tail: one sqrt, two quotients

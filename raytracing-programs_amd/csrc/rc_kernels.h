@@ -38,6 +38,8 @@ struct ParityWork {
   void* cin;                // [P]   resolved carry-in per DEP entry (CinG tagged granules)
   int* counters;            // [16]  nseg, head, ndep, ordered, phase-C tickets, census, ...
   int* batch_state;         // [P/64+1] phase-C batch claim words (0 free, 1 claimed)
+  int* batch_cnt;           // [P/64+1] entries of each batch with a published carry-in
+  int* batch_rq;            // [P/64+1] batches in the order they became complete (+1; 0 empty)
   hipStream_t side;         // phase C's side stream (null: phase C after the resolver only)
   hipEvent_t fork, join;    // side stream waits on fork; the main stream waits on join
   int side_blocks;          // resident k_side workgroups
@@ -103,15 +105,19 @@ hipError_t launch_shard_local(const LaunchScene& s, int W, int H, int row0, int 
                               hipStream_t stream);
 // The root: image scan order from the gathered rows ([G][rmax]) and entries (rank g's at
 // offs[g]), the carry resolver, and the carry-ins in the gathered layout (cin_ret).
-// ev (optional): [0] resolver start, [1] resolver end.
+// ev (optional): [0] resolver start, [1] resolver end.  bound: entries delivered per rank
+// (the fixed-size exchange; beyond it a rank's list is not read as records).
 hipError_t launch_shard_resolve(const LaunchScene& s, int W, int H, int G, int rmax,
                                 const void* rows_all, const void* ent_all,
                                 const long long* offs, int maxrec, const ParityWork& w,
-                                void* cin_ret, hipStream_t stream, const hipEvent_t* ev);
+                                void* cin_ret, hipStream_t stream, const hipEvent_t* ev,
+                                int bound = 0x7fffffff);
 // A rank: phase C of its DEP list once its carry-ins (tag) are in w.cin.
+// limit: carry-ins exist for the first `limit` entries only (fixed-size exchange)
 hipError_t launch_shard_phase_c(const LaunchScene& s, int W, int H, int row0, int row_step,
                                 int maxrec, uint8_t* out, const ParityWork& w, unsigned tag,
-                                unsigned long long* zcount, hipStream_t stream);
+                                unsigned long long* zcount, hipStream_t stream,
+                                int limit = 0x7fffffff);
 // The root: image <- gathered row blocks [G][rmax][W*3].
 hipError_t launch_deinterleave(const uint8_t* gathered, int G, int rmax, int W, int H,
                                uint8_t* img, hipStream_t stream);

@@ -901,10 +901,17 @@ __global__ void __launch_bounds__(1024) k_seg_order(const int* __restrict__ seg_
                                                      int* __restrict__ counters,
                                                      int* __restrict__ order,
                                                      int* __restrict__ batch_state,
+                                                     int* __restrict__ batch_cnt,
+                                                     int* __restrict__ batch_rq,
                                                      int block_min) {
   const int nseg = counters[0], ndep = counters[2];
-  // phase C's per-batch claim words (64 DEP entries per batch), zeroed for this frame
-  for (int b = threadIdx.x; b < (ndep + 63) / 64; b += blockDim.x) batch_state[b] = 0;
+  // phase C's per-batch claim words (64 DEP entries per batch), completion counts and ready
+  // queue, zeroed for this frame
+  for (int b = threadIdx.x; b < (ndep + 63) / 64; b += blockDim.x) {
+    batch_state[b] = 0;
+    batch_cnt[b] = 0;
+    batch_rq[b] = 0;
+  }
   if (nseg > kSegOrderMax) {
     if (threadIdx.x == 0) {
       counters[3] = 0;
@@ -1225,7 +1232,10 @@ struct TeamState {
   int err_block;
   int err_info;
   int err_info2;
-  int pad[28];
+  // phase C's ready queue (lone frames with k_side): batches pushed as they complete, taken
+  // by k_side's waves in that order (ready_range, phase_c_ready)
+  int rq_prod, rq_cons;
+  int pad[26];
   TeamSlot slot[2][kTeamMax];
   DenseQueue dq;
 };
@@ -1249,6 +1259,40 @@ __device__ __forceinline__ bool spin_expired(TeamState* ts, unsigned long long t
   if (dt > kSpinLimit) return true;
   return dt > kSpinPoll &&
          __hip_atomic_load(&ts->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+}
+
+// Phase C's ready queue.  Entries [j0, j1) of the DEP list have their carry-ins published:
+// credit them to their 64-entry batches; a batch whose every entry is credited is pushed to
+// the queue, so k_side shades batches in the order they complete instead of waiting on them
+// in index order (the team's segment holds the first 844k entries at quadric 4096^2 and
+// resolves last: index order left 70 % of phase C for after the resolver).  Ranges credited
+// by the resolver partition the DEP list, so every batch is pushed exactly once.  A batch
+// lying wholly inside the range needs no count.  One wave; every lane calls it.
+__device__ __forceinline__ void ready_range(int* __restrict__ cnt, int* __restrict__ rq,
+                                            TeamState* ts, int ndep, int j0, int j1) {
+  if (!cnt || j0 >= j1) return;
+  const int lane = threadIdx.x & 63;
+  const int b0 = j0 >> 6, b1 = (j1 - 1) >> 6;
+  for (int bb = b0; bb <= b1; bb += 64) {
+    const int b = bb + lane;
+    bool done = false;
+    if (b <= b1) {
+      const int lo = j0 > b * 64 ? j0 : b * 64;
+      const int hi = j1 < b * 64 + 64 ? j1 : b * 64 + 64;
+      const int size = (ndep < b * 64 + 64 ? ndep : b * 64 + 64) - b * 64;
+      const int add = hi - lo;
+      done = add == size || atomicAdd(&cnt[b], add) + add == size;
+    }
+    const unsigned long long m = __ballot(done);
+    if (m) {
+      int k0 = 0;
+      if (lane == 0) k0 = atomicAdd(&ts->rq_prod, __popcll(m));
+      k0 = __shfl(k0, 0, 64);
+      if (done)
+        __hip_atomic_store(&rq[k0 + __popcll(m & lanemask_lt())], b + 1, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
 }
 
 __device__ __forceinline__ void team_publish(TeamState* ts, int round, unsigned pos, V3 c) {
@@ -1297,7 +1341,8 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
     int* __restrict__ counters, int* __restrict__ head,
     CinG* __restrict__ cin, int team_blocks, int long_len, TeamState* __restrict__ ts,
     unsigned* __restrict__ trace, int G, int wave_k, int resolve_k, unsigned tag,
-    int helpers, int hand_run, int inject, int block_min) {
+    int helpers, int hand_run, int inject, int block_min, int* __restrict__ rq_cnt,
+    int* __restrict__ rq) {
   // census for phase C's side kernel: it only proceeds once every resolver block is resident
   if (threadIdx.x == 0)
     __hip_atomic_fetch_add(&counters[5], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1485,6 +1530,10 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
           resolve = false;
           __syncthreads();
         }
+        // the round's entries [j_round, j) are published: the team's last block credits them
+        // to phase C's ready queue (off the leader's chain)
+        if ((int)blockIdx.x == T - 1 && wave == 0)
+          ready_range(rq_cnt, rq, ts, ndep, j_round, j < end ? j : end);
         // debug trace: per-round team log after the per-segment records and stamps
         if (trace && blockIdx.x == 0 && wave == 0 && lane == 0 && round < 8192) {
           unsigned* tl = trace + 3 * (size_t)ndep + 4 * (size_t)nseg + 8 * (size_t)round;
@@ -1589,6 +1638,7 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
         if (j + t < end) s_bw.rec[t] = nxt;
         __syncthreads();
       }
+      if (wave == 0) ready_range(rq_cnt, rq, ts, ndep, j_item, end);
       if (trace && t == 0 && k < 64) {   // debug trace: the helper's items
         unsigned* ti = trace + 3 * (size_t)ndep + 5 * (size_t)nseg + 8 * 8192 + 4096 + 16384 + 8 * k;
         ti[0] = (unsigned)sg;
@@ -1659,6 +1709,7 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
         if (j + t < end) s_bw.rec[t] = nxt;
         __syncthreads();
       }
+      if (wave == 0) ready_range(rq_cnt, rq, ts, ndep, start, end);
       if (trace && t == 0) {
         trace[3 * sg] = (unsigned)(__builtin_amdgcn_s_memrealtime() - t_seg);
 #if RC_STAMPS   // LANE passes << 16 | cooperative steps (block windows)
@@ -1673,15 +1724,32 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
   }
 
   // ------------------------------------------------------------- regular waves --
+  // A regular workgroup's waves take their first segments together: four consecutive ones
+  // of the length-ordered queue.  The longest segments then sit in a few workgroups (lone
+  // quadric 4096^2: ~100 segments of 2.5-4.2 ms land on ~25 workgroups instead of one wave in
+  // each of ~100), and the others vacate their CUs as soon as the short segments are gone —
+  // k_side shades phase C on vacated CUs only.
+  __shared__ int s_first;
+  int first = -1;
+  if ((int)blockIdx.x >= team_blocks + helpers) {
+    if (threadIdx.x == 0) s_first = atomicAdd(headb, kResolveBlock / 64);
+    __syncthreads();
+    first = s_first + wave;
+  }
   for (;;) {
     int s = 0;
     if (lane == 0) {
-      s = atomicAdd(headb, 1);
-      if (s >= nseg) {   // head B is done: any long segment no workgroup has taken yet
-        s = atomicAdd(head, 1);
-        if (s >= nlong) s = nseg;
+      if (first >= 0 && first < nseg) {
+        s = first;
+      } else {
+        s = atomicAdd(headb, 1);
+        if (s >= nseg) {   // head B is done: any long segment no workgroup has taken yet
+          s = atomicAdd(head, 1);
+          if (s >= nlong) s = nseg;
+        }
       }
     }
+    first = -1;
     s = __shfl(s, 0, 64);
     if (s >= nseg) break;
     if (ordered) s = seg_order[s];
@@ -1713,6 +1781,8 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
         const unsigned long long hm = __ballot(j + lane < end && mhit);
         cin_put_wave(cin, j, 0, end - j < 64 ? end - j : 64, mine, tag, hm,
                      reinterpret_cast<float*>(&s_bw) + wave * 192);
+        // phase C may shade these entries now (a window touches at most two batches)
+        ready_range(rq_cnt, rq, ts, ndep, j, end - j < 64 ? end : j + 64);
       }
       // a long run of changers: hand the rest of the segment to a helper block (15 carry
       // guesses per step instead of this wave's 3)
@@ -1929,14 +1999,72 @@ __device__ __forceinline__ void phase_c_passes(const Scene& sc, const Cam& cam, 
   }
 }
 
+// Phase C beside the resolver: batches in the order they complete (the resolver's ready
+// queue, ready_range).  Item k of the queue exists once k batches have completed; every
+// batch completes by the resolver's end, so a wave waiting for item k < nb is waiting for
+// resolver progress (bounded: a lack of progress for 5 s, or an error raised elsewhere).
+// k_finish takes whatever these waves have not claimed.
+__device__ __forceinline__ void phase_c_ready(const Scene& sc, const Cam& cam, int W,
+                                              int maxrec, const long long* __restrict__ dep_pix,
+                                              const DepRec* __restrict__ deprec,
+                                              const float4* __restrict__ pcol,
+                                              CinG* __restrict__ cin, int* __restrict__ counters,
+                                              int* __restrict__ batch_state,
+                                              const int* __restrict__ rq, uint8_t* __restrict__ out,
+                                              uint32_t* __restrict__ patch, TeamState* ts,
+                                              unsigned tag, int& zero,
+                                              unsigned* __restrict__ trace) {
+  const int ndep = counters[2];
+  const int nb = (ndep + 63) / 64;
+  unsigned* tq = trace ? trace + 3 * (size_t)ndep + 5 * (size_t)counters[0] + 200000 : nullptr;
+  for (;;) {
+    const int k = wave_ticket(&ts->rq_cons);
+    if (k >= nb) break;
+    if (tq && (threadIdx.x & 63) == 0) tq[3 * k] = (unsigned)__builtin_amdgcn_s_memrealtime();
+    int b = -1;
+    if ((threadIdx.x & 63) == 0) {
+      unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+      int seen = -1;
+      for (;;) {
+        const int v = __hip_atomic_load(&rq[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (v) {
+          b = v - 1;
+          break;
+        }
+        const int prod = __hip_atomic_load(&ts->rq_prod, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (prod != seen) {
+          seen = prod;
+          t0 = __builtin_amdgcn_s_memrealtime();
+        } else if (spin_expired(ts, t0)) {   // the batch's carries are k_finish's to wait for
+          break;
+        }
+        __builtin_amdgcn_s_sleep(32);
+      }
+    }
+    b = __shfl(b, 0, 64);
+    if (b < 0) break;
+    int mine = 0;
+    if ((threadIdx.x & 63) == 0) mine = batch_claim(batch_state, b);
+    if (!__shfl(mine, 0, 64)) continue;
+    V3 c = v3(0.0f, 0.0f, 0.0f);
+    bool hit = true;
+    if (tq && (threadIdx.x & 63) == 0) tq[3 * k + 1] = (unsigned)__builtin_amdgcn_s_memrealtime();
+    (void)batch_carries(cin, ndep, b, tag, true, c, hit, ts);   // published: arrives at once
+    shade_batch(sc, cam, W, maxrec, dep_pix, deprec, pcol, ndep, b, c, hit, out, patch, zero);
+    if ((threadIdx.x & 63) == 0) atomicAdd(&counters[9], 1);
+    if (tq && (threadIdx.x & 63) == 0) tq[3 * k + 2] = (unsigned)__builtin_amdgcn_s_memrealtime();
+  }
+}
+
 template <bool kStage>
 __global__ void __launch_bounds__(kSideBlock) k_side(
     Scene sc, Cam cam, int W, int H, int maxrec, const uint8_t* __restrict__ cls,
     const long long* __restrict__ dep_pix, const DepRec* __restrict__ deprec,
     const float4* __restrict__ pcol, CinG* __restrict__ cin, int* __restrict__ counters,
-    int* __restrict__ batch_state, uint8_t* __restrict__ out, uint32_t* __restrict__ patch,
-    unsigned long long* __restrict__ zcount, TeamState* __restrict__ ts, int resolve_blocks,
-    unsigned tag, int tiles) {
+    int* __restrict__ batch_state, const int* __restrict__ rq, uint8_t* __restrict__ out,
+    uint32_t* __restrict__ patch, unsigned long long* __restrict__ zcount,
+    TeamState* __restrict__ ts, int resolve_blocks, unsigned tag, int tiles,
+    unsigned* __restrict__ trace) {
   __shared__ int s_go;
   __shared__ StageBuf<kStage> stage;
   stage_scene<kStage>(sc, stage);
@@ -1971,8 +2099,8 @@ __global__ void __launch_bounds__(kSideBlock) k_side(
     shade_tile(sc, cam, W, H, maxrec, t, cls, out, zero);
     if ((threadIdx.x & 63) == 0) atomicAdd(&counters[8], 1);
   }
-  phase_c_passes(sc, cam, W, maxrec, dep_pix, deprec, pcol, cin, counters, batch_state, out, patch, ts, tag, true,
-                 zero);
+  phase_c_ready(sc, cam, W, maxrec, dep_pix, deprec, pcol, cin, counters, batch_state, rq, out,
+                patch, ts, tag, zero, trace);
   flush_events(zero, zcount);
 }
 
@@ -1987,7 +2115,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_
     const float4* __restrict__ pcol, CinG* __restrict__ cin, int* __restrict__ counters,
     int* __restrict__ batch_state, uint8_t* __restrict__ out, uint32_t* __restrict__ patch,
     unsigned long long* __restrict__ zcount, TeamState* __restrict__ ts, unsigned tag,
-    int tiles) {
+    int tiles, const int* __restrict__ rq) {
   __shared__ StageBuf<kStage> stage;
   stage_scene<kStage>(sc, stage);
   int zero = 0;
@@ -1998,6 +2126,12 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_
     shade_tile(sc, cam, W, H, maxrec, t, cls, out, zero);
     if ((threadIdx.x & 63) == 0) atomicAdd(&counters[10], 1);
   }
+  // with k_side: the ready queue's remaining items first (every batch has completed when this
+  // kernel runs: the last ones are the resolver's final rounds, shaded here at full occupancy
+  // instead of by k_side's one workgroup per CU), then anything still unclaimed
+  if (rq)
+    phase_c_ready(sc, cam, W, maxrec, dep_pix, deprec, pcol, cin, counters, batch_state, rq,
+                  out, patch, ts, tag, zero, nullptr);
   phase_c_passes(sc, cam, W, maxrec, dep_pix, deprec, pcol, cin, counters, batch_state, out, patch, ts, tag, false,
                  zero);
   flush_events(zero, zcount);
@@ -2024,13 +2158,16 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_
     const long long* __restrict__ dep_pix,
     const DepRec* __restrict__ deprec, const float4* __restrict__ pcol, CinG* __restrict__ cin,
     const int* __restrict__ counters, uint8_t* __restrict__ out, uint32_t* __restrict__ patch,
-    unsigned long long* __restrict__ zcount, TeamState* __restrict__ ts, unsigned tag) {
+    unsigned long long* __restrict__ zcount, TeamState* __restrict__ ts, unsigned tag,
+    int limit) {
   __shared__ StageBuf<kStage> stage;
   __shared__ int s_j[kChunk];
   __shared__ float s_c[kChunk][3];
   __shared__ int s_n;
   stage_scene<kStage>(sc, stage);
-  const int ndep = counters[2];
+  // limit: a row shard's fixed-size exchange delivered carry-ins for its first `limit` entries
+  // only (the frame is rendered again when the count exceeds it, rc_shard.hip)
+  const int ndep = counters[2] < limit ? counters[2] : limit;
   const int nchunks = (ndep + kChunk - 1) / kChunk;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   int zero = 0;
@@ -2191,7 +2328,7 @@ __global__ void __launch_bounds__(256) k_shard_unpack(
     const int* __restrict__ row_soff, const long long* __restrict__ row_prevw,
     const long long* __restrict__ row_prevd, DepRec* __restrict__ deprec,
     long long* __restrict__ dep_pix, int* __restrict__ seg_start,
-    long long* __restrict__ seg_key, float4* __restrict__ keycarry) {
+    long long* __restrict__ seg_key, float4* __restrict__ keycarry, int bound) {
   const int y = blockIdx.x * kRowWaves + (int)(threadIdx.x >> 6);
   if (y >= H) return;
   const int lane = threadIdx.x & 63;
@@ -2214,7 +2351,15 @@ __global__ void __launch_bounds__(256) k_shard_unpack(
     const bool valid = i < n;
     ShardEntry q;
     if (valid) q = e[i];
-    const long long pix = valid ? (long long)q.rec.pad : -1;
+    // bound: the fixed-size exchange delivered each rank's first `bound` entries.  A longer
+    // list (the frame is then rendered again, rc_shard.hip) reads the next rank's block: such
+    // an entry becomes a harmless record (zero directions, shape 0) continuing its segment,
+    // never an out-of-range shape index for the resolver
+    if (valid && r.loff + i >= bound) {
+      q.rec = DepRec{0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0, -1, 0.0f, 0.0f, 0.0f, -1};
+      q.kc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    }
+    const long long pix = valid ? (q.rec.pad >= 0 ? (long long)q.rec.pad : pd) : -1;
     const long long kin = valid ? (long long)q.rec.pad2 : -1;
     long long prev = __shfl_up(pix, 1, 64);
     if (lane == 0) prev = pd;
@@ -2353,7 +2498,7 @@ hipError_t launch_parity(const LaunchScene& s, int W, int H, int maxrec, uint8_t
                      w.row_off, w.row_soff, w.row_prevw, w.row_prevd, w.dep_pix, w.seg_start,
                      w.seg_key);
   hipLaunchKernelGGL(k_seg_order, dim3(1), dim3(1024), 0, stream, w.seg_start, w.counters,
-                     w.seg_order, w.batch_state, w.block_min);
+                     w.seg_order, w.batch_state, w.batch_cnt, w.batch_rq, w.block_min);
   // resolve_lds > 80 KiB keeps one resolver block (4 waves, one per SIMD) per CU: the chain
   // steps are latency-bound, so a resolver wave should not share its SIMD
   if (ev) (void)hipEventRecord(ev[1], stream);
@@ -2370,7 +2515,8 @@ hipError_t launch_parity(const LaunchScene& s, int W, int H, int maxrec, uint8_t
                      maxrec, (const DepRec*)w.deprec, w.dep_pix, w.seg_key, w.wcarry,
                      w.seg_start, w.seg_order, w.counters, w.counters + 1, (CinG*)w.cin, w.team_blocks,
                      w.long_len, (TeamState*)w.team, w.trace, w.coop_group, w.wave_k,
-                     w.resolve_k, w.epoch, w.helpers, w.hand_run, w.inject, w.block_min);
+                     w.resolve_k, w.epoch, w.helpers, w.hand_run, w.inject, w.block_min,
+                     w.side ? w.batch_cnt : nullptr, w.batch_rq);
   if (w.rstream) {
     if (w.rt1) (void)hipEventRecord(w.rt1, rs);
     (void)hipEventRecord(w.rdone, rs);
@@ -2383,9 +2529,9 @@ hipError_t launch_parity(const LaunchScene& s, int W, int H, int maxrec, uint8_t
     hipLaunchKernelGGL(st ? k_side<true> : k_side<false>, dim3(w.side_blocks), dim3(kSideBlock), w.side_lds, w.side, sc, cam,
                        W, H, maxrec, w.cls, w.dep_pix, (const DepRec*)w.deprec, w.wcarry,
                        (CinG*)w.cin, w.counters,
-                       w.batch_state,
+                       w.batch_state, w.batch_rq,
                        out, w.patch, zcount, (TeamState*)w.team, w.resolve_blocks, w.epoch,
-                       w.split_shade);
+                       w.split_shade, w.trace);
     (void)hipEventRecord(w.join, w.side);
   }
   if (ev) (void)hipEventRecord(ev[2], stream);
@@ -2411,13 +2557,15 @@ static void enqueue_phase_c(const Scene& sc, const Cam& cam, bool st, int W, int
                        maxrec, w.cls, w.dep_pix, (const DepRec*)w.deprec, w.wcarry,
                        (CinG*)w.cin, w.counters, w.batch_state,
                        out, w.patch,
-                       zcount, (TeamState*)w.team, w.epoch, (w.side && w.split_shade) ? 1 : 0);
+                       zcount, (TeamState*)w.team, w.epoch, (w.side && w.split_shade) ? 1 : 0,
+                       w.side ? w.batch_rq : nullptr);
   } else {   // all of phase C after the resolver: clean entries, then full waves of the rest
     hipLaunchKernelGGL((sc.dep_fast ? (st ? k_dep_chunks<true, true> : k_dep_chunks<false, true>)
                                : (st ? k_dep_chunks<true, false> : k_dep_chunks<false, false>)), dim3(w.phase_c_blocks),
                        dim3(kBlock), 0, stream, sc, cam, W, 0, 1, maxrec, w.dep_pix,
                        (const DepRec*)w.deprec, (const float4*)w.wcarry, (CinG*)w.cin,
-                       w.counters, out, w.patch, zcount, (TeamState*)w.team, w.epoch);
+                       w.counters, out, w.patch, zcount, (TeamState*)w.team, w.epoch,
+                       0x7fffffff);
   }
 }
 
@@ -2514,7 +2662,8 @@ hipError_t launch_shard_local(const LaunchScene& s, int W, int H, int row0, int 
 hipError_t launch_shard_resolve(const LaunchScene& s, int W, int H, int G, int rmax,
                                 const void* rows_all, const void* ent_all,
                                 const long long* offs, int maxrec, const ParityWork& w,
-                                void* cin_ret, hipStream_t stream, const hipEvent_t* ev) {
+                                void* cin_ret, hipStream_t stream, const hipEvent_t* ev,
+                                int bound) {
   if (G < 1 || G > kMaxShards) return hipErrorInvalidValue;
   const Scene sc = make_scene(s);
   ShardOffs o{};
@@ -2530,16 +2679,17 @@ hipError_t launch_shard_resolve(const LaunchScene& s, int W, int H, int G, int r
   hipLaunchKernelGGL(k_shard_unpack, dim3(row_blocks), dim3(256), 0, stream, rs,
                      (const ShardEntry*)ent_all, o, G, rmax, W, H, w.row_off, w.row_soff,
                      w.row_prevw, w.row_prevd, (DepRec*)w.deprec, w.dep_pix, w.seg_start,
-                     w.seg_key, w.wcarry);
+                     w.seg_key, w.wcarry, bound);
   hipLaunchKernelGGL(k_seg_order, dim3(1), dim3(1024), 0, stream, w.seg_start, w.counters,
-                     w.seg_order, w.batch_state, w.block_min);
+                     w.seg_order, w.batch_state, w.batch_cnt, w.batch_rq, w.block_min);
   if (ev) (void)hipEventRecord(ev[0], stream);
   auto kres = s.n <= kLdsShapes ? k_resolve<true> : k_resolve<false>;
   hipLaunchKernelGGL(kres, dim3(w.resolve_blocks), dim3(kResolveBlock), w.resolve_lds, stream,
                      sc, maxrec, (const DepRec*)w.deprec, w.dep_pix, w.seg_key, w.wcarry,
                      w.seg_start, w.seg_order, w.counters, w.counters + 1, (CinG*)w.cin,
                      w.team_blocks, w.long_len, (TeamState*)w.team, w.trace, w.coop_group,
-                     w.wave_k, w.resolve_k, w.epoch, w.helpers, w.hand_run, w.inject, w.block_min);
+                     w.wave_k, w.resolve_k, w.epoch, w.helpers, w.hand_run, w.inject, w.block_min,
+                     w.side ? w.batch_cnt : nullptr, w.batch_rq);
   if (ev) (void)hipEventRecord(ev[1], stream);
   hipLaunchKernelGGL(k_shard_cin, dim3(row_blocks), dim3(256), 0, stream, rs, o, G, rmax, H,
                      w.row_off, (const CinG*)w.cin, (CinG*)cin_ret);
@@ -2548,7 +2698,7 @@ hipError_t launch_shard_resolve(const LaunchScene& s, int W, int H, int G, int r
 
 hipError_t launch_shard_phase_c(const LaunchScene& s, int W, int H, int row0, int row_step,
                                 int maxrec, uint8_t* out, const ParityWork& w, unsigned tag,
-                                unsigned long long* zcount, hipStream_t stream) {
+                                unsigned long long* zcount, hipStream_t stream, int limit) {
   const Scene sc = make_scene(s);
   const Cam cam = make_cam(s, W, H);
   hipLaunchKernelGGL((s.dep_fast ? (stage_fits(s) ? k_dep_chunks<true, true> : k_dep_chunks<false, true>)
@@ -2556,7 +2706,7 @@ hipError_t launch_shard_phase_c(const LaunchScene& s, int W, int H, int row0, in
                      dim3(w.phase_c_blocks), dim3(kBlock), 0, stream, sc, cam, W, row0, row_step,
                      maxrec, w.dep_pix, (const DepRec*)w.deprec, (const float4*)w.wcarry,
                      (CinG*)w.cin, w.counters, out, (uint32_t*)nullptr, zcount,
-                     (TeamState*)w.team, tag);
+                     (TeamState*)w.team, tag, limit);
   return hipGetLastError();
 }
 

@@ -80,6 +80,14 @@ struct rc_group {
   Rank* root = nullptr;                       // rank 0 when this process drives it
   unsigned epoch = 0;                         // carry-in tag of the last sharded parity frame
   rc_shard_stats last{};
+  // Fixed-size entry exchange (no host synchronisation inside a frame): the DEP entries per
+  // rank of the last frame with this key, an upper bound for the next one.  A frame whose
+  // count exceeds it is detected at the frame's end and rendered again with exact sizes.
+  struct {
+    const void* scene = nullptr;
+    int W = 0, H = 0, maxrec = 0;
+    long long per_rank = -1;
+  } bound;
 };
 
 namespace {
@@ -241,6 +249,23 @@ int scatter_var(rc_group& g, const void* send, const std::vector<void*>& recv,
   return 0;
 }
 
+// rank r's recv <- root.send[r * bytes ..] (every rank receives `bytes`)
+int scatter_fixed(rc_group& g, const void* send, const std::vector<void*>& recv, size_t bytes) {
+  if (g.transport == RC_XFER_RCCL) {
+    NCCL_TRY(ncclGroupStart());
+    for (size_t i = 0; i < g.ranks.size(); ++i) {
+      Rank& r = *g.ranks[i];
+      NCCL_TRY(ncclScatter(r.rank == 0 ? send : nullptr, recv[i], bytes, ncclUint8, 0, r.comm,
+                           r.stream));
+    }
+    NCCL_TRY(ncclGroupEnd());
+    return 0;
+  }
+  std::vector<size_t> off(g.nranks), by(g.nranks, bytes);
+  for (int q = 0; q < g.nranks; ++q) off[q] = (size_t)q * bytes;
+  return scatter_var(g, send, recv, off, by);
+}
+
 int sync_all(rc_group& g) {
   for (auto& rp : g.ranks) {
     HIP_TRY(hipSetDevice(rp->device));
@@ -292,9 +317,10 @@ int render_sharded(rc_group& g, const rc_scene* s, int W, int H, const rc_option
                                   zc, r.stream, opt->mode == RC_MODE_CUDA));
       continue;
     }
-    const int lrows = r.nrows > 0 ? r.nrows : 1;
-    if (ensure_parity(*r.c, r.fb, W, lrows, w[i], r.c->cus) ||
-        r.ent.ensure((size_t)lrows * W * rc::shard_entry_bytes()) ||
+    // workspace for rmax rows on every rank: the fixed-size exchange moves the same number of
+    // entries (up to the bound, <= rmax * W) out of and into every rank's buffers
+    if (ensure_parity(*r.c, r.fb, W, rmax, w[i], r.c->cus) ||
+        r.ent.ensure((size_t)rmax * W * rc::shard_entry_bytes()) ||
         r.rows.ensure((size_t)rmax * rc::shard_row_bytes())) {
       std::fprintf(stderr, "Error: out of device memory for the shard workspace\n");
       return -1;
@@ -305,6 +331,10 @@ int render_sharded(rc_group& g, const rc_scene* s, int W, int H, const rc_option
                            r.stream));
   }
   if (root) HIP_TRY(hipEventRecord(root->ev[1], root->stream));
+  // fixed-size exchange when the last frame with this key bounds the entry counts
+  const bool fixed = parity && g.bound.per_rank >= 0 && g.bound.scene == s->img &&
+                     g.bound.W == W && g.bound.H == H && g.bound.maxrec == maxrec;
+  std::vector<size_t> cnt(G, 0);
   if (parity) {
     // 2. row summaries and entry counts to the root
     std::vector<const void*> sr, sc;
@@ -316,18 +346,22 @@ int render_sharded(rc_group& g, const rc_scene* s, int W, int H, const rc_option
     if (gather_fixed(g, sr, root ? root->rows_all.p : nullptr, (size_t)rmax * rc::shard_row_bytes()) ||
         gather_fixed(g, sc, root ? root->small_all.p : nullptr, 16))
       return -1;
-    for (auto& rp : g.ranks) {
-      HIP_TRY(hipSetDevice(rp->device));
-      HIP_TRY(hipMemcpyAsync(rp->h_small, rp->small.p, 16, hipMemcpyDeviceToHost, rp->stream));
+    std::vector<size_t> off(G, 0), eb(G), eo(G), cb(G), co(G);
+    if (fixed) {   // every rank's list padded to the bound: sizes known without the counts
+      for (int q = 0; q < G; ++q) cnt[q] = (size_t)g.bound.per_rank;
+    } else {   // the counts first (host synchronisation), then the exact sizes
+      for (auto& rp : g.ranks) {
+        HIP_TRY(hipSetDevice(rp->device));
+        HIP_TRY(hipMemcpyAsync(rp->h_small, rp->small.p, 16, hipMemcpyDeviceToHost, rp->stream));
+      }
+      if (root)
+        HIP_TRY(hipMemcpyAsync(root->h_small_all, root->small_all.p, (size_t)G * 16,
+                               hipMemcpyDeviceToHost, root->stream));
+      if (sync_all(g)) return -1;
+      for (auto& rp : g.ranks) rp->ndep = rp->h_small[0];
+      for (int q = 0; q < G; ++q) cnt[q] = root ? (size_t)root->h_small_all[4 * q] : 0;
+      for (auto& rp : g.ranks) cnt[rp->rank] = (size_t)rp->ndep;
     }
-    if (root)
-      HIP_TRY(hipMemcpyAsync(root->h_small_all, root->small_all.p, (size_t)G * 16,
-                             hipMemcpyDeviceToHost, root->stream));
-    if (sync_all(g)) return -1;
-    std::vector<size_t> cnt(G, 0), off(G, 0), eb(G), eo(G), cb(G), co(G);
-    for (auto& rp : g.ranks) rp->ndep = rp->h_small[0];
-    for (int q = 0; q < G; ++q) cnt[q] = root ? (size_t)root->h_small_all[4 * q] : 0;
-    for (auto& rp : g.ranks) cnt[rp->rank] = (size_t)rp->ndep;
     size_t total = 0;
     for (int q = 0; q < G; ++q) {
       off[q] = total;
@@ -347,8 +381,12 @@ int render_sharded(rc_group& g, const rc_scene* s, int W, int H, const rc_option
       HIP_TRY(hipSetDevice(root->device));
       root->rootfb.epoch = g.epoch - 1;
       root->rootfb.scene_src = s->img;   // the resolver's evaluator is specialised by shape count
-      if (root->ent_all.ensure(total * rc::shard_entry_bytes() + 64) ||
-          root->cin_ret.ensure(total * (size_t)rc::kCinBytes + 64) ||
+      // capacity for every rank's largest possible list (rmax * W): with the fixed-size
+      // exchange a list longer than the bound is read (as garbage, the frame is rendered
+      // again) beyond its block, never beyond the buffer
+      const size_t cap = total > (size_t)G * rmax * W ? total : (size_t)G * rmax * W;
+      if (root->ent_all.ensure(cap * rc::shard_entry_bytes() + 64) ||
+          root->cin_ret.ensure(cap * (size_t)rc::kCinBytes + 64) ||
           ensure_parity(*root->c, root->rootfb, W, H, wr, root->c->cus)) {
         std::fprintf(stderr, "Error: out of device memory for the root's resolver workspace\n");
         return -1;
@@ -359,25 +397,30 @@ int render_sharded(rc_group& g, const rc_scene* s, int W, int H, const rc_option
     }
     std::vector<const void*> se;
     for (auto& rp : g.ranks) se.push_back(rp->ent.p);
-    if (gather_var(g, se, root ? root->ent_all.p : nullptr, eo, eb)) return -1;
+    if (fixed ? gather_fixed(g, se, root ? root->ent_all.p : nullptr, eb[0])
+              : gather_var(g, se, root ? root->ent_all.p : nullptr, eo, eb))
+      return -1;
     if (root) {
       HIP_TRY(hipSetDevice(root->device));
       std::vector<long long> offs(off.begin(), off.end());
       hipEvent_t rev[2] = {root->ev[2], root->ev[3]};
       HIP_TRY(rc::launch_shard_resolve(ls[0], W, H, G, rmax, root->rows_all.p, root->ent_all.p,
                                        offs.data(), maxrec, wr, root->cin_ret.p, root->stream,
-                                       rev));
+                                       rev, fixed ? (int)g.bound.per_rank : 0x7fffffff));
     }
     std::vector<void*> rcv;
     for (size_t i = 0; i < g.ranks.size(); ++i) rcv.push_back(w[i].cin);
-    if (scatter_var(g, root ? root->cin_ret.p : nullptr, rcv, co, cb)) return -1;
+    if (fixed ? scatter_fixed(g, root ? root->cin_ret.p : nullptr, rcv, cb[0])
+              : scatter_var(g, root ? root->cin_ret.p : nullptr, rcv, co, cb))
+      return -1;
     // 4. every rank: phase C of its entries
     for (size_t i = 0; i < g.ranks.size(); ++i) {
       Rank& r = *g.ranks[i];
-      if (!r.ndep) continue;
+      if (!fixed && !r.ndep) continue;   // (fixed: the count is on the device only)
       HIP_TRY(hipSetDevice(r.device));
       HIP_TRY(rc::launch_shard_phase_c(ls[i], W, H, r.rank, G, maxrec, (uint8_t*)r.frame.p, w[i],
-                                       g.epoch, (unsigned long long*)r.fb.zcount.p, r.stream));
+                                       g.epoch, (unsigned long long*)r.fb.zcount.p, r.stream,
+                                       fixed ? (int)g.bound.per_rank : 0x7fffffff));
     }
   }
   if (root) HIP_TRY(hipEventRecord(root->ev[4], root->stream));
@@ -401,12 +444,46 @@ int render_sharded(rc_group& g, const rc_scene* s, int W, int H, const rc_option
                            hipMemcpyDeviceToHost, root->stream));
     HIP_TRY(hipEventRecord(root->ev[5], root->stream));
   }
+  if (parity) {
+    // every rank learns the frame's largest entry count (small[4]): the bound of the next
+    // frame with this key, and the check of this one's (all ranks decide alike)
+    if (g.transport == RC_XFER_RCCL) {
+      NCCL_TRY(ncclGroupStart());
+      for (auto& rp : g.ranks)
+        NCCL_TRY(ncclAllReduce(rp->small.p, (int*)rp->small.p + 4, 1, ncclInt32, ncclMax,
+                               rp->comm, rp->stream));
+      NCCL_TRY(ncclGroupEnd());
+    }
+    for (auto& rp : g.ranks) {
+      HIP_TRY(hipSetDevice(rp->device));
+      HIP_TRY(hipMemcpyAsync(rp->h_small, rp->small.p, 32, hipMemcpyDeviceToHost, rp->stream));
+    }
+  }
   if (sync_all(g)) return -1;
   int rc = 0;
   if (parity) {
     for (auto& rp : g.ranks)
       if (rp->fb.team.p && report_spin_error(rp->fb, "shard phase C")) rc = -1;
     if (root && report_spin_error(root->rootfb, "shard resolver")) rc = -1;
+  }
+  if (parity) {
+    // the largest entry count of the frame (RCCL: the all-reduce; device copies: every rank is
+    // in this process), identical on every rank
+    long long mx = 0;
+    for (auto& rp : g.ranks) {
+      const long long n = g.transport == RC_XFER_RCCL ? (long long)rp->h_small[4]
+                                                      : (long long)rp->h_small[0];
+      if (n > mx) mx = n;
+    }
+    if (fixed && mx > g.bound.per_rank) {   // an entry list overflowed the padded exchange
+      g.bound.per_rank = -1;
+      return 1;   // render_sharded_retry renders the frame again with exact sizes
+    }
+    g.bound.scene = s->img;
+    g.bound.W = W;
+    g.bound.H = H;
+    g.bound.maxrec = maxrec;
+    g.bound.per_rank = mx;
   }
   rc_shard_stats& st = g.last;
   std::memset(&st, 0, sizeof st);
@@ -442,6 +519,15 @@ int render_sharded(rc_group& g, const rc_scene* s, int W, int H, const rc_option
   return rc;
 }
 
+// A frame whose DEP entries overflowed the fixed-size exchange (render_sharded returns 1, on
+// every rank alike) is rendered again with exact sizes.
+int render_sharded_retry(rc_group& g, const rc_scene* s, int W, int H, const rc_options* opt,
+                         uint8_t* d_image, rc_timing* timing) {
+  int rc = render_sharded(g, s, W, H, opt, d_image, timing);
+  if (rc == 1) rc = render_sharded(g, s, W, H, opt, d_image, timing);
+  return rc;
+}
+
 // Lock every driven device (ascending order: no lock-order inversion between groups).
 struct DeviceLocks {
   std::vector<std::unique_lock<std::mutex>> held;
@@ -473,7 +559,7 @@ int render_local_group(int first, int n, const rc_scene* s, int W, int H, const 
     c_n = n;
   }
   DeviceLocks locks(*cached);
-  if (render_sharded(*cached, s, W, H, opt, nullptr, timing)) return -1;
+  if (render_sharded_retry(*cached, s, W, H, opt, nullptr, timing)) return -1;
   *d_image = (uint8_t*)cached->root->image.p;
   return 0;
 }
@@ -568,10 +654,16 @@ int rc_render_sharded(rc_group* g, const rc_scene* s, int W, int H, const rc_opt
   int rc;
   {
     DeviceLocks locks(*g);
-    rc = render_sharded(*g, s, W, H, opt, d_image, timing);
+    rc = render_sharded_retry(*g, s, W, H, opt, d_image, timing);
   }
   (void)hipSetDevice(dev);
   return rc;
+}
+
+int rc_group_debug_bound(rc_group* g, long long per_rank) {
+  if (!g || per_rank < -1) return -1;
+  g->bound.per_rank = per_rank;
+  return 0;
 }
 
 int rc_group_last_stats(const rc_group* g, rc_shard_stats* out) {

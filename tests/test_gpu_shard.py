@@ -157,3 +157,20 @@ def test_sharded_cuda_mode(G, scenes):
             np.testing.assert_array_equal(sharded(g, scenes[name], 160, 97, d, "cuda"),
                                           oracle_render_cuda(scenes[name], 160, 97, d),
                                           err_msg=f"{name} d{d} G{G}")
+
+
+@pytest.mark.parametrize("G", [1, 3, 8])
+def test_sharded_fixed_exchange(G, scenes, table):
+    """Repeated frames of one scene and size exchange the DEP entries in fixed-size per-rank
+    blocks (no host synchronisation inside the frame, the bound from the previous frame); a
+    frame whose entries overflow the bound is rendered again with exact sizes.  Every image
+    md5-equal, for the exact, the fixed and the overflowed-then-exact frames."""
+    g = group([0] * G, "copy")
+    key = "quadric:1024x1024:d6:parity"
+    want = table[key]["md5"]
+    for i in range(3):   # exact (new key), then fixed twice
+        assert p3_md5(sharded(g, scenes["quadric"], 1024, 1024, 6, "parity")) == want, i
+    g.debug_bound(16)    # far below the real count: the next frame overflows, then renders exact
+    assert p3_md5(sharded(g, scenes["quadric"], 1024, 1024, 6, "parity")) == want, "overflow"
+    assert p3_md5(sharded(g, scenes["quadric"], 1024, 1024, 6, "parity")) == want, "after"
+    g.debug_bound(-1)
