@@ -241,8 +241,9 @@ int rc_profile_end(rc_phase_stats *out);
  * top of it.  Takes effect at the next render (the frame pipeline's layout at its next
  * build: rc_pipe_reset). */
 typedef struct rc_tuning {
-  int side;               /* a lone parity frame's phase C beside the resolver: 0 never,  
-                             1 always, 2 for images of >= 8 Mpixel (default)              */
+  int side;               /* a lone parity frame's phase C: 0 after the resolver, 1 beside
+                             it (k_side), 2 beside it for images of >= 8 Mpixel, 3 inside
+                             the resolver (its idle waves shade ready batches; default)   */
   int split_shade;        /* 1: phase A's colours move beside the resolver (needs side)    */
   int resolve_shared;     /* 1: no one-resolver-workgroup-per-CU LDS reservation           */
   int resolve_lds_kb;     /* resolver LDS reservation in KiB, 0 = by path (96 / 56)        */

@@ -36,7 +36,7 @@ std::mutex g_ctx_mu;
 
 rc_tuning default_tuning() {
   rc_tuning t;
-  t.side = 2;
+  t.side = 3;
   t.split_shade = 0;
   t.resolve_shared = 0;
   t.resolve_lds_kb = 0;
@@ -360,7 +360,7 @@ int rc_set_tuning(const rc_tuning* t) {
   if (!t) return -1;
   auto in = [](int v, int lo, int hi) { return v >= lo && v <= hi; };
   const bool ok =
-      in(t->side, 0, 2) && in(t->split_shade, 0, 1) && in(t->resolve_shared, 0, 1) &&
+      in(t->side, 0, 3) && in(t->split_shade, 0, 1) && in(t->resolve_shared, 0, 1) &&
       in(t->resolve_lds_kb, 0, 152) && (t->resolve_grid == 0 || in(t->resolve_grid, 8, 1 << 16)) &&
       in(t->team_blocks, -1, 256) && in(t->helpers, 0, rc::kDenseSlots) &&
       in(t->hand_run, 1, 1 << 30) && in(t->long_len, 64, 1 << 30) && in(t->wave_k, 1, 64) &&
@@ -583,6 +583,9 @@ int ensure_parity(DevCtx& c, FrameBufs& b, int W, int H, rc::ParityWork& w, int 
     }
   }
   if (!w.side) w.split_shade = 0;   // split shading needs the side kernel
+  // side 3: phase C inside the resolver (its waves shade ready batches once their own work is
+  // done), a lone frame only
+  w.inres = (!piped && tu.side == 3) ? 1 : 0;
   w.epoch = b.epoch;
   w.counters = (int*)b.counters.p;
   w.team = b.team.p;
@@ -691,6 +694,11 @@ int enqueue_render_ws(DevCtx& c, const rc_scene* s, int W, int H, int row0, int 
     return -1;
   }
   if (w.split_shade) ls.dep_fast = 0;   // k_classify leaves no primary shade
+  // phase C inside the resolver needs a resolver long enough to hide it: at depth 1 (two
+  // levels) the chains are short and the resolver's one wave per SIMD shades more slowly than
+  // k_dep_chunks' full occupancy (simple 1024^2 d1 0.143 -> 0.175 ms; from depth 2 it gains:
+  // 1024^2 d6 0.678 -> 0.663, reflection 2048^2 d4 0.966 -> 0.873, quadric 4096^2 5.58 -> 5.18)
+  if (maxrec < 3) w.inres = 0;
   w.patch = patch;
   w.inject = take_inject();
   HIP_TRY(rc::launch_parity(ls, W, H, maxrec, d_out, w, zc, stream, timed ? ev + 1 : nullptr));

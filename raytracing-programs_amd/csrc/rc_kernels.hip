@@ -1332,6 +1332,239 @@ __device__ __forceinline__ bool team_collect(TeamState* ts, int round, int b, un
   }
 }
 
+// ------------------------------------------------------------------ parity phase C --
+// Colours and phase C beside the resolver.  k_classify leaves every colour to be shaded: the
+// non-DEP pixels (8x8 tiles, always ready) and the DEP pixels with their resolved carry-ins,
+// in batches of 64 consecutive DEP entries (one per lane).  k_side runs them on a second
+// stream while the resolver runs, on the CUs the resolver's workgroups have left (its LDS
+// reservation cannot fit beside one: side_lds_bytes; sharing the SIMDs slows the chains and,
+// above all, the team's rounds): tiles first, then phase C pass 1 (batches whose carry-ins
+// are already published — tagged granules, CinG) and pass 2 (everything not yet claimed,
+// waiting for it).  k_finish, after the resolver on the main stream, claims what is left.
+// A batch is shaded exactly once: its claim word goes 0 -> 1 by an agent-scope CAS; tiles
+// are claimed from one counter.
+constexpr int kSideBlock = 256;
+
+__device__ __forceinline__ bool batch_claim(int* state, int b) {
+  int expect = 0;
+  return __hip_atomic_compare_exchange_strong(&state[b], &expect, 1, __ATOMIC_RELAXED,
+                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Loads batch b's carry-ins; false if `wait` is false and one is not published yet.
+__device__ __forceinline__ bool batch_carries(CinG* cin, int ndep, int b, unsigned tag,
+                                              bool wait, V3& c, bool& hit, TeamState* ts) {
+  const int j = b * 64 + (int)(threadIdx.x & 63);
+  // Only the lanes whose carry-in is still missing poll again (a lane keeps a complete entry),
+  // and the poll interval grows: while the resolver runs, phase C's waiting waves would
+  // otherwise re-read whole batches of agent-scope granules every microsecond and load the
+  // memory fabric the resolver's own hand-offs go through (lone frame: resolver 4.65 ms
+  // beside the waiting side kernel vs 4.48 ms alone).
+  // The limit measures a lack of progress (ADVICE r1): it restarts whenever another of the
+  // batch's carry-ins arrives or another regular resolver wave finishes, so a legitimately
+  // long resolver (huge frames, scenes whose shapes are not staged in LDS) is not cut off.
+  bool ok = j >= ndep;
+  unsigned long long t0 = 0;
+  int seen = -1;
+  for (int poll = 0;; ++poll) {
+    if (!ok) ok = cin_get(cin, j, tag, c, hit);
+    if (__all(ok)) return true;
+    if (!wait) return false;
+    const int progress =
+        __popcll(__ballot(ok)) +
+        __hip_atomic_load(&ts->dq.finished, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (progress != seen) {
+      seen = progress;
+      t0 = __builtin_amdgcn_s_memrealtime();
+    } else if (spin_expired(ts, t0)) {
+      // the first entry of the batch that is still missing
+      const unsigned long long miss = __ballot(!ok);
+      if ((threadIdx.x & 63) == 0) set_error(ts, 2, b * 64 + (__ffsll((long long)miss) - 1), ndep);
+      return true;
+    }
+    if (poll < 4) __builtin_amdgcn_s_sleep(32);
+    else __builtin_amdgcn_s_sleep(127);
+  }
+}
+
+// Phase C of one batch of 64 DEP entries.  Under dep_fast phase A left each entry's primary
+// shade in wcarry[p] and counted the events of its primary part: a clean entry (no level hit
+// at its carry-in) is exactly that shade (every level's shade is zero, C/raycast.c:366-378),
+// the others resume at level 2 (shade_dep_cont).  Otherwise the pixel is recomputed.
+__device__ __forceinline__ void shade_batch(const Scene& sc, const Cam& cam, int W, int maxrec,
+                                            const long long* __restrict__ dep_pix,
+                                            const DepRec* __restrict__ deprec,
+                                            const float4* __restrict__ pcol, int ndep, int b,
+                                            V3 c, bool hit, uint8_t* __restrict__ out,
+                                            uint32_t* __restrict__ patch, int& zero) {
+  const int j = b * 64 + (int)(threadIdx.x & 63);
+  if (j >= ndep) return;
+  const long long p = dep_pix[j];
+  if (sc.dep_fast) {
+    V3 rgb;
+    if (hit) {
+      rgb = shade_dep_cont(sc, deprec[p], maxrec, c, pcol + p, zero);
+    } else {
+      const float4 k = pcol[p];
+      rgb = v3(k.x, k.y, k.z);
+    }
+    store_dep(out, patch, p, j, rgb);
+    return;
+  }
+  const int y = (int)(p / W), x = (int)(p % W);
+  const V3 d = primary_dir(cam, x, y, zero);
+  PixelOut po;
+  shoot<kModeParityC>(sc, d, maxrec, c, po, zero);
+  store_dep(out, patch, p, j, po.rgb);
+}
+
+__device__ __forceinline__ int wave_ticket(int* ctr) {
+  int b = 0;
+  if ((threadIdx.x & 63) == 0) b = atomicAdd(ctr, 1);
+  return __shfl(b, 0, 64);
+}
+
+// Shading of one 8x8 tile's non-DEP pixels (phase A's colour part, events counted).
+__device__ __forceinline__ void shade_tile(const Scene& sc, const Cam& cam, int W, int H,
+                                           int maxrec, int t, const uint8_t* __restrict__ cls,
+                                           uint8_t* __restrict__ out, int& zero) {
+  const int tw = (W + 7) >> 3;
+  const int lane = threadIdx.x & 63;
+  const int x = (t % tw) * 8 + (lane & 7), y = (t / tw) * 8 + (lane >> 3);
+  if (x >= W || y >= H) return;
+  const size_t p = (size_t)y * W + x;
+  if (cls[p] == kClsDep) return;
+  const V3 d = primary_dir(cam, x, y, zero);
+  PixelOut po;
+  shoot<kModeParityA>(sc, d, maxrec, v3(0.0f, 0.0f, 0.0f), po, zero);
+  store_rgb(out + p * 3, po.rgb);
+}
+
+// Phase C pass 1 (published batches) and pass 2 (everything unclaimed, waiting).
+__device__ __forceinline__ void phase_c_passes(const Scene& sc, const Cam& cam, int W,
+                                               int maxrec, const long long* __restrict__ dep_pix,
+                                               const DepRec* __restrict__ deprec,
+                                               const float4* __restrict__ pcol,
+                                               CinG* __restrict__ cin, int* __restrict__ counters,
+                                               int* __restrict__ batch_state,
+                                               uint8_t* __restrict__ out,
+                                               uint32_t* __restrict__ patch, TeamState* ts,
+                                               unsigned tag, bool pass1, int& zero) {
+  int* done_ctr = &counters[pass1 ? 9 : 11];
+  const int ndep = counters[2];
+  const int nb = (ndep + 63) / 64;
+  while (pass1) {
+    const int b = wave_ticket(&counters[4]);
+    if (b >= nb) break;
+    // one granule first: the batch's last entry (most batches are still unpublished in this
+    // pass; probing all 192 granules of each would put ~1.5 KB of agent-scope loads per batch
+    // on the fabric the resolver's hand-offs use)
+    {
+      const int jl = (b * 64 + 63 < ndep ? b * 64 + 63 : ndep - 1);
+      const unsigned long long g0 =
+          __hip_atomic_load(&cin[jl].g[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (((unsigned)(g0 >> 32) & ~kCinHit) != tag) continue;
+    }
+    V3 c = v3(0.0f, 0.0f, 0.0f);
+    bool hit = true;
+    if (!batch_carries(cin, ndep, b, tag, false, c, hit, ts)) continue;
+    int mine = 0;
+    if ((threadIdx.x & 63) == 0) mine = batch_claim(batch_state, b);
+    if (!__shfl(mine, 0, 64)) continue;
+    shade_batch(sc, cam, W, maxrec, dep_pix, deprec, pcol, ndep, b, c, hit, out, patch, zero);
+    if ((threadIdx.x & 63) == 0) atomicAdd(done_ctr, 1);
+  }
+  for (;;) {
+    const int b = wave_ticket(&counters[6]);
+    if (b >= nb) break;
+    int mine = 0;
+    if ((threadIdx.x & 63) == 0) mine = batch_claim(batch_state, b);
+    if (!__shfl(mine, 0, 64)) continue;
+    V3 c = v3(0.0f, 0.0f, 0.0f);
+    bool hit = true;
+    (void)batch_carries(cin, ndep, b, tag, true, c, hit, ts);
+    shade_batch(sc, cam, W, maxrec, dep_pix, deprec, pcol, ndep, b, c, hit, out, patch, zero);
+    if ((threadIdx.x & 63) == 0) atomicAdd(done_ctr, 1);
+  }
+}
+
+// Phase C beside the resolver: batches in the order they complete (the resolver's ready
+// queue, ready_range).  Item k of the queue exists once k batches have completed; every
+// batch completes by the resolver's end, so a wave waiting for item k < nb is waiting for
+// resolver progress (bounded: a lack of progress for 5 s, or an error raised elsewhere).
+// k_finish takes whatever these waves have not claimed.
+__device__ __forceinline__ void phase_c_ready(const Scene& sc, const Cam& cam, int W,
+                                              int maxrec, const long long* __restrict__ dep_pix,
+                                              const DepRec* __restrict__ deprec,
+                                              const float4* __restrict__ pcol,
+                                              CinG* __restrict__ cin, int* __restrict__ counters,
+                                              int* __restrict__ batch_state,
+                                              const int* __restrict__ rq, uint8_t* __restrict__ out,
+                                              uint32_t* __restrict__ patch, TeamState* ts,
+                                              unsigned tag, int& zero,
+                                              unsigned* __restrict__ trace) {
+  const int ndep = counters[2];
+  const int nb = (ndep + 63) / 64;
+  unsigned* tq = trace ? trace + 3 * (size_t)ndep + 5 * (size_t)counters[0] + 200000 : nullptr;
+  for (;;) {
+    const int k = wave_ticket(&ts->rq_cons);
+    if (k >= nb) break;
+    if (tq && (threadIdx.x & 63) == 0) tq[3 * k] = (unsigned)__builtin_amdgcn_s_memrealtime();
+    int b = -1;
+    if ((threadIdx.x & 63) == 0) {
+      unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+      int seen = -1;
+      for (;;) {
+        const int v = __hip_atomic_load(&rq[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (v) {
+          b = v - 1;
+          break;
+        }
+        const int prod = __hip_atomic_load(&ts->rq_prod, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (prod != seen) {
+          seen = prod;
+          t0 = __builtin_amdgcn_s_memrealtime();
+        } else if (spin_expired(ts, t0)) {   // the batch's carries are k_finish's to wait for
+          break;
+        }
+        __builtin_amdgcn_s_sleep(32);
+      }
+    }
+    b = __shfl(b, 0, 64);
+    if (b < 0) break;
+    int mine = 0;
+    if ((threadIdx.x & 63) == 0) mine = batch_claim(batch_state, b);
+    if (!__shfl(mine, 0, 64)) continue;
+    V3 c = v3(0.0f, 0.0f, 0.0f);
+    bool hit = true;
+    if (tq && (threadIdx.x & 63) == 0) tq[3 * k + 1] = (unsigned)__builtin_amdgcn_s_memrealtime();
+    (void)batch_carries(cin, ndep, b, tag, true, c, hit, ts);   // published: arrives at once
+    shade_batch(sc, cam, W, maxrec, dep_pix, deprec, pcol, ndep, b, c, hit, out, patch, zero);
+    if ((threadIdx.x & 63) == 0) atomicAdd(&counters[9], 1);
+    if (tq && (threadIdx.x & 63) == 0) tq[3 * k + 2] = (unsigned)__builtin_amdgcn_s_memrealtime();
+  }
+}
+
+// Phase C inside the resolver (rc_tuning.side 3): a resolver wave whose own work is done (no
+// segment left to take, no hand-off left for a helper) shades batches from the ready queue
+// instead of leaving its SIMD idle; k_finish, after the resolver, finds the queue drained.
+__device__ __forceinline__ void resolver_phase_c(const Scene& sc, const Cam& cam, int W, int maxrec,
+                                              const long long* __restrict__ dep_pix,
+                                              const DepRec* __restrict__ deprec,
+                                              const float4* __restrict__ pcol,
+                                              CinG* __restrict__ cin, int* __restrict__ counters,
+                                              int* __restrict__ batch_state,
+                                              const int* __restrict__ rq,
+                                              uint8_t* __restrict__ out,
+                                              uint32_t* __restrict__ patch,
+                                              unsigned long long* __restrict__ zcount,
+                                              TeamState* ts, unsigned tag) {
+  int zero = 0;
+  phase_c_ready(sc, cam, W, maxrec, dep_pix, deprec, pcol, cin, counters, batch_state, rq, out,
+                patch, ts, tag, zero, nullptr);
+  flush_events(zero, zcount);
+}
+
 template <bool kLds>
 __global__ void __launch_bounds__(kResolveBlock) k_resolve(
     Scene sc, int maxrec, const DepRec* __restrict__ deprec,
@@ -1342,7 +1575,8 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
     CinG* __restrict__ cin, int team_blocks, int long_len, TeamState* __restrict__ ts,
     unsigned* __restrict__ trace, int G, int wave_k, int resolve_k, unsigned tag,
     int helpers, int hand_run, int inject, int block_min, int* __restrict__ rq_cnt,
-    int* __restrict__ rq) {
+    int* __restrict__ rq, Cam cam, int W, uint8_t* __restrict__ out, uint32_t* __restrict__ patch,
+    unsigned long long* __restrict__ zcount, int* __restrict__ batch_state, int inres) {
   // census for phase C's side kernel: it only proceeds once every resolver block is resident
   if (threadIdx.x == 0)
     __hip_atomic_fetch_add(&counters[5], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1657,6 +1891,8 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
     if (trace && lane == 0)   // debug trace: when each wave leaves
       trace[3 * (size_t)ndep + 5 * (size_t)nseg + 8 * 8192 + blockIdx.x * 4 + wave] =
           (unsigned)__builtin_amdgcn_s_memrealtime();
+    if (inres) resolver_phase_c(sc, cam, W, maxrec, dep_pix, deprec, wcarry, cin, counters,
+                                batch_state, rq, out, patch, zcount, ts, tag);
     return;   // helpers take no regular segments
   }
 
@@ -1841,221 +2077,9 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
   if (trace && lane == 0)   // debug trace: when each wave leaves
     trace[3 * (size_t)ndep + 5 * (size_t)nseg + 8 * 8192 + blockIdx.x * 4 + wave] =
         (unsigned)__builtin_amdgcn_s_memrealtime();
+  if (inres) resolver_phase_c(sc, cam, W, maxrec, dep_pix, deprec, wcarry, cin, counters,
+                              batch_state, rq, out, patch, zcount, ts, tag);
 }
-
-// ------------------------------------------------------------------ parity phase C --
-// Colours and phase C beside the resolver.  k_classify leaves every colour to be shaded: the
-// non-DEP pixels (8x8 tiles, always ready) and the DEP pixels with their resolved carry-ins,
-// in batches of 64 consecutive DEP entries (one per lane).  k_side runs them on a second
-// stream while the resolver runs, on the CUs the resolver's workgroups have left (its LDS
-// reservation cannot fit beside one: side_lds_bytes; sharing the SIMDs slows the chains and,
-// above all, the team's rounds): tiles first, then phase C pass 1 (batches whose carry-ins
-// are already published — tagged granules, CinG) and pass 2 (everything not yet claimed,
-// waiting for it).  k_finish, after the resolver on the main stream, claims what is left.
-// A batch is shaded exactly once: its claim word goes 0 -> 1 by an agent-scope CAS; tiles
-// are claimed from one counter.
-constexpr int kSideBlock = 256;
-
-__device__ __forceinline__ bool batch_claim(int* state, int b) {
-  int expect = 0;
-  return __hip_atomic_compare_exchange_strong(&state[b], &expect, 1, __ATOMIC_RELAXED,
-                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Loads batch b's carry-ins; false if `wait` is false and one is not published yet.
-__device__ __forceinline__ bool batch_carries(CinG* cin, int ndep, int b, unsigned tag,
-                                              bool wait, V3& c, bool& hit, TeamState* ts) {
-  const int j = b * 64 + (int)(threadIdx.x & 63);
-  // Only the lanes whose carry-in is still missing poll again (a lane keeps a complete entry),
-  // and the poll interval grows: while the resolver runs, phase C's waiting waves would
-  // otherwise re-read whole batches of agent-scope granules every microsecond and load the
-  // memory fabric the resolver's own hand-offs go through (lone frame: resolver 4.65 ms
-  // beside the waiting side kernel vs 4.48 ms alone).
-  // The limit measures a lack of progress (ADVICE r1): it restarts whenever another of the
-  // batch's carry-ins arrives or another regular resolver wave finishes, so a legitimately
-  // long resolver (huge frames, scenes whose shapes are not staged in LDS) is not cut off.
-  bool ok = j >= ndep;
-  unsigned long long t0 = 0;
-  int seen = -1;
-  for (int poll = 0;; ++poll) {
-    if (!ok) ok = cin_get(cin, j, tag, c, hit);
-    if (__all(ok)) return true;
-    if (!wait) return false;
-    const int progress =
-        __popcll(__ballot(ok)) +
-        __hip_atomic_load(&ts->dq.finished, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (progress != seen) {
-      seen = progress;
-      t0 = __builtin_amdgcn_s_memrealtime();
-    } else if (spin_expired(ts, t0)) {
-      // the first entry of the batch that is still missing
-      const unsigned long long miss = __ballot(!ok);
-      if ((threadIdx.x & 63) == 0) set_error(ts, 2, b * 64 + (__ffsll((long long)miss) - 1), ndep);
-      return true;
-    }
-    if (poll < 4) __builtin_amdgcn_s_sleep(32);
-    else __builtin_amdgcn_s_sleep(127);
-  }
-}
-
-// Phase C of one batch of 64 DEP entries.  Under dep_fast phase A left each entry's primary
-// shade in wcarry[p] and counted the events of its primary part: a clean entry (no level hit
-// at its carry-in) is exactly that shade (every level's shade is zero, C/raycast.c:366-378),
-// the others resume at level 2 (shade_dep_cont).  Otherwise the pixel is recomputed.
-__device__ __forceinline__ void shade_batch(const Scene& sc, const Cam& cam, int W, int maxrec,
-                                            const long long* __restrict__ dep_pix,
-                                            const DepRec* __restrict__ deprec,
-                                            const float4* __restrict__ pcol, int ndep, int b,
-                                            V3 c, bool hit, uint8_t* __restrict__ out,
-                                            uint32_t* __restrict__ patch, int& zero) {
-  const int j = b * 64 + (int)(threadIdx.x & 63);
-  if (j >= ndep) return;
-  const long long p = dep_pix[j];
-  if (sc.dep_fast) {
-    V3 rgb;
-    if (hit) {
-      rgb = shade_dep_cont(sc, deprec[p], maxrec, c, pcol + p, zero);
-    } else {
-      const float4 k = pcol[p];
-      rgb = v3(k.x, k.y, k.z);
-    }
-    store_dep(out, patch, p, j, rgb);
-    return;
-  }
-  const int y = (int)(p / W), x = (int)(p % W);
-  const V3 d = primary_dir(cam, x, y, zero);
-  PixelOut po;
-  shoot<kModeParityC>(sc, d, maxrec, c, po, zero);
-  store_dep(out, patch, p, j, po.rgb);
-}
-
-__device__ __forceinline__ int wave_ticket(int* ctr) {
-  int b = 0;
-  if ((threadIdx.x & 63) == 0) b = atomicAdd(ctr, 1);
-  return __shfl(b, 0, 64);
-}
-
-// Shading of one 8x8 tile's non-DEP pixels (phase A's colour part, events counted).
-__device__ __forceinline__ void shade_tile(const Scene& sc, const Cam& cam, int W, int H,
-                                           int maxrec, int t, const uint8_t* __restrict__ cls,
-                                           uint8_t* __restrict__ out, int& zero) {
-  const int tw = (W + 7) >> 3;
-  const int lane = threadIdx.x & 63;
-  const int x = (t % tw) * 8 + (lane & 7), y = (t / tw) * 8 + (lane >> 3);
-  if (x >= W || y >= H) return;
-  const size_t p = (size_t)y * W + x;
-  if (cls[p] == kClsDep) return;
-  const V3 d = primary_dir(cam, x, y, zero);
-  PixelOut po;
-  shoot<kModeParityA>(sc, d, maxrec, v3(0.0f, 0.0f, 0.0f), po, zero);
-  store_rgb(out + p * 3, po.rgb);
-}
-
-// Phase C pass 1 (published batches) and pass 2 (everything unclaimed, waiting).
-__device__ __forceinline__ void phase_c_passes(const Scene& sc, const Cam& cam, int W,
-                                               int maxrec, const long long* __restrict__ dep_pix,
-                                               const DepRec* __restrict__ deprec,
-                                               const float4* __restrict__ pcol,
-                                               CinG* __restrict__ cin, int* __restrict__ counters,
-                                               int* __restrict__ batch_state,
-                                               uint8_t* __restrict__ out,
-                                               uint32_t* __restrict__ patch, TeamState* ts,
-                                               unsigned tag, bool pass1, int& zero) {
-  int* done_ctr = &counters[pass1 ? 9 : 11];
-  const int ndep = counters[2];
-  const int nb = (ndep + 63) / 64;
-  while (pass1) {
-    const int b = wave_ticket(&counters[4]);
-    if (b >= nb) break;
-    // one granule first: the batch's last entry (most batches are still unpublished in this
-    // pass; probing all 192 granules of each would put ~1.5 KB of agent-scope loads per batch
-    // on the fabric the resolver's hand-offs use)
-    {
-      const int jl = (b * 64 + 63 < ndep ? b * 64 + 63 : ndep - 1);
-      const unsigned long long g0 =
-          __hip_atomic_load(&cin[jl].g[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (((unsigned)(g0 >> 32) & ~kCinHit) != tag) continue;
-    }
-    V3 c = v3(0.0f, 0.0f, 0.0f);
-    bool hit = true;
-    if (!batch_carries(cin, ndep, b, tag, false, c, hit, ts)) continue;
-    int mine = 0;
-    if ((threadIdx.x & 63) == 0) mine = batch_claim(batch_state, b);
-    if (!__shfl(mine, 0, 64)) continue;
-    shade_batch(sc, cam, W, maxrec, dep_pix, deprec, pcol, ndep, b, c, hit, out, patch, zero);
-    if ((threadIdx.x & 63) == 0) atomicAdd(done_ctr, 1);
-  }
-  for (;;) {
-    const int b = wave_ticket(&counters[6]);
-    if (b >= nb) break;
-    int mine = 0;
-    if ((threadIdx.x & 63) == 0) mine = batch_claim(batch_state, b);
-    if (!__shfl(mine, 0, 64)) continue;
-    V3 c = v3(0.0f, 0.0f, 0.0f);
-    bool hit = true;
-    (void)batch_carries(cin, ndep, b, tag, true, c, hit, ts);
-    shade_batch(sc, cam, W, maxrec, dep_pix, deprec, pcol, ndep, b, c, hit, out, patch, zero);
-    if ((threadIdx.x & 63) == 0) atomicAdd(done_ctr, 1);
-  }
-}
-
-// Phase C beside the resolver: batches in the order they complete (the resolver's ready
-// queue, ready_range).  Item k of the queue exists once k batches have completed; every
-// batch completes by the resolver's end, so a wave waiting for item k < nb is waiting for
-// resolver progress (bounded: a lack of progress for 5 s, or an error raised elsewhere).
-// k_finish takes whatever these waves have not claimed.
-__device__ __forceinline__ void phase_c_ready(const Scene& sc, const Cam& cam, int W,
-                                              int maxrec, const long long* __restrict__ dep_pix,
-                                              const DepRec* __restrict__ deprec,
-                                              const float4* __restrict__ pcol,
-                                              CinG* __restrict__ cin, int* __restrict__ counters,
-                                              int* __restrict__ batch_state,
-                                              const int* __restrict__ rq, uint8_t* __restrict__ out,
-                                              uint32_t* __restrict__ patch, TeamState* ts,
-                                              unsigned tag, int& zero,
-                                              unsigned* __restrict__ trace) {
-  const int ndep = counters[2];
-  const int nb = (ndep + 63) / 64;
-  unsigned* tq = trace ? trace + 3 * (size_t)ndep + 5 * (size_t)counters[0] + 200000 : nullptr;
-  for (;;) {
-    const int k = wave_ticket(&ts->rq_cons);
-    if (k >= nb) break;
-    if (tq && (threadIdx.x & 63) == 0) tq[3 * k] = (unsigned)__builtin_amdgcn_s_memrealtime();
-    int b = -1;
-    if ((threadIdx.x & 63) == 0) {
-      unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-      int seen = -1;
-      for (;;) {
-        const int v = __hip_atomic_load(&rq[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (v) {
-          b = v - 1;
-          break;
-        }
-        const int prod = __hip_atomic_load(&ts->rq_prod, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (prod != seen) {
-          seen = prod;
-          t0 = __builtin_amdgcn_s_memrealtime();
-        } else if (spin_expired(ts, t0)) {   // the batch's carries are k_finish's to wait for
-          break;
-        }
-        __builtin_amdgcn_s_sleep(32);
-      }
-    }
-    b = __shfl(b, 0, 64);
-    if (b < 0) break;
-    int mine = 0;
-    if ((threadIdx.x & 63) == 0) mine = batch_claim(batch_state, b);
-    if (!__shfl(mine, 0, 64)) continue;
-    V3 c = v3(0.0f, 0.0f, 0.0f);
-    bool hit = true;
-    if (tq && (threadIdx.x & 63) == 0) tq[3 * k + 1] = (unsigned)__builtin_amdgcn_s_memrealtime();
-    (void)batch_carries(cin, ndep, b, tag, true, c, hit, ts);   // published: arrives at once
-    shade_batch(sc, cam, W, maxrec, dep_pix, deprec, pcol, ndep, b, c, hit, out, patch, zero);
-    if ((threadIdx.x & 63) == 0) atomicAdd(&counters[9], 1);
-    if (tq && (threadIdx.x & 63) == 0) tq[3 * k + 2] = (unsigned)__builtin_amdgcn_s_memrealtime();
-  }
-}
-
 template <bool kStage>
 __global__ void __launch_bounds__(kSideBlock) k_side(
     Scene sc, Cam cam, int W, int H, int maxrec, const uint8_t* __restrict__ cls,
@@ -2116,6 +2140,12 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_
     int* __restrict__ batch_state, uint8_t* __restrict__ out, uint32_t* __restrict__ patch,
     unsigned long long* __restrict__ zcount, TeamState* __restrict__ ts, unsigned tag,
     int tiles, const int* __restrict__ rq) {
+  // every batch already shaded through the ready queue (the usual case when the resolver's
+  // own waves shade them): nothing to stage or claim
+  if (rq && !tiles &&
+      __hip_atomic_load(&counters[9], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >=
+          (counters[2] + 63) / 64)
+    return;
   __shared__ StageBuf<kStage> stage;
   stage_scene<kStage>(sc, stage);
   int zero = 0;
@@ -2516,7 +2546,8 @@ hipError_t launch_parity(const LaunchScene& s, int W, int H, int maxrec, uint8_t
                      w.seg_start, w.seg_order, w.counters, w.counters + 1, (CinG*)w.cin, w.team_blocks,
                      w.long_len, (TeamState*)w.team, w.trace, w.coop_group, w.wave_k,
                      w.resolve_k, w.epoch, w.helpers, w.hand_run, w.inject, w.block_min,
-                     w.side ? w.batch_cnt : nullptr, w.batch_rq);
+                     (w.side || w.inres) ? w.batch_cnt : nullptr, w.batch_rq, cam, W, out,
+                     w.patch, zcount, w.batch_state, w.inres);
   if (w.rstream) {
     if (w.rt1) (void)hipEventRecord(w.rt1, rs);
     (void)hipEventRecord(w.rdone, rs);
@@ -2552,13 +2583,13 @@ hipError_t launch_phase_c(const LaunchScene& s, int W, int H, int maxrec, uint8_
 static void enqueue_phase_c(const Scene& sc, const Cam& cam, bool st, int W, int H, int maxrec,
                             uint8_t* out, const ParityWork& w, unsigned long long* zcount,
                             hipStream_t stream) {
-  if (w.side || w.phase_c_finish) {   // what k_side has not claimed (or the claim-based form)
+  if (w.side || w.inres || w.phase_c_finish) {   // what k_side / the resolver's waves left
     hipLaunchKernelGGL(st ? k_finish<true> : k_finish<false>, dim3(w.phase_c_blocks), dim3(kBlock), 0, stream, sc, cam, W, H,
                        maxrec, w.cls, w.dep_pix, (const DepRec*)w.deprec, w.wcarry,
                        (CinG*)w.cin, w.counters, w.batch_state,
                        out, w.patch,
                        zcount, (TeamState*)w.team, w.epoch, (w.side && w.split_shade) ? 1 : 0,
-                       w.side ? w.batch_rq : nullptr);
+                       (w.side || w.inres) ? w.batch_rq : nullptr);
   } else {   // all of phase C after the resolver: clean entries, then full waves of the rest
     hipLaunchKernelGGL((sc.dep_fast ? (st ? k_dep_chunks<true, true> : k_dep_chunks<false, true>)
                                : (st ? k_dep_chunks<true, false> : k_dep_chunks<false, false>)), dim3(w.phase_c_blocks),
@@ -2689,7 +2720,8 @@ hipError_t launch_shard_resolve(const LaunchScene& s, int W, int H, int G, int r
                      w.seg_start, w.seg_order, w.counters, w.counters + 1, (CinG*)w.cin,
                      w.team_blocks, w.long_len, (TeamState*)w.team, w.trace, w.coop_group,
                      w.wave_k, w.resolve_k, w.epoch, w.helpers, w.hand_run, w.inject, w.block_min,
-                     w.side ? w.batch_cnt : nullptr, w.batch_rq);
+                     nullptr, w.batch_rq, make_cam(s, W, H), W, nullptr, nullptr, nullptr,
+                     nullptr, 0);
   if (ev) (void)hipEventRecord(ev[1], stream);
   hipLaunchKernelGGL(k_shard_cin, dim3(row_blocks), dim3(256), 0, stream, rs, o, G, rmax, H,
                      w.row_off, (const CinG*)w.cin, (CinG*)cin_ret);

@@ -57,7 +57,9 @@ def test_configs(key, scenes, table):
     assert p3_md5(img) == table[key]["md5"], key
 
 
-SCHEDULES = {"no-side": dict(side=0), "side-always": dict(side=1),
+SCHEDULES = {"no-side": dict(side=0), "side-always": dict(side=1), "side-by-size": dict(side=2),
+             "in-resolver+no-dep-fast": dict(side=3, dep_fast=0),
+             "in-resolver+no-helpers": dict(side=3, helpers=0),
              "split-shade": dict(split_shade=1, side=1),
              "resolve-shared": dict(resolve_shared=1), "no-dep-fast": dict(dep_fast=0),
              "no-side+no-dep-fast": dict(side=0, dep_fast=0),
@@ -115,7 +117,7 @@ ZERO_EVENT_PLANES = [((0, 0, 1), 0.5, ""), ((0, 0.6, 0.8), 0.5, ""), ((0, 0.28, 
 
 @pytest.mark.parametrize("case", range(len(ZERO_EVENT_PLANES)))
 @pytest.mark.parametrize("fast_dep", [True, False])
-@pytest.mark.parametrize("side", [True, False])
+@pytest.mark.parametrize("side", [0, 1, 3])
 def test_zero_normalize_events(case, fast_dep, side, tmp_path):
     """Zero-length normalize events (C/v3math.c:183-187; raycast() prints one stderr line per
     event): a point light exactly on the hit point of the 1x1 image's ray.  The pixel is a
@@ -130,8 +132,8 @@ def test_zero_normalize_events(case, fast_dep, side, tmp_path):
                     "light, color: [4, 4, 4], radial-a2: 0.01, radial-a1: 0.0125, "
                     "radial-a0: 0.0125, position: [0, 0, -5]\n")
     s = rc.Scene.from_file(str(path))
-    # side=0: phase C after the resolver (k_dep_chunks)
-    with rc.tuned(dep_fast=int(fast_dep), side=int(side)):
+    # side=0: phase C after the resolver (k_dep_chunks); 1: k_side; 3: the resolver's waves
+    with rc.tuned(dep_fast=int(fast_dep), side=side):
         for w, h in ((1, 1), (2, 1), (3, 1), (1, 3)):
             want, st = oracle_render(s, w, h, 6, "parity")
             tim = {}
