@@ -243,7 +243,8 @@ int rc_profile_end(rc_phase_stats *out);
 typedef struct rc_tuning {
   int side;               /* a lone parity frame's phase C: 0 after the resolver, 1 beside
                              it (k_side), 2 beside it for images of >= 8 Mpixel, 3 inside
-                             the resolver (its idle waves shade ready batches; default)   */
+                             the resolver (its idle waves shade ready batches; default), 4
+                             inside it until its own work is over (k_finish: the rest)    */
   int split_shade;        /* 1: phase A's colours move beside the resolver (needs side)    */
   int resolve_shared;     /* 1: no one-resolver-workgroup-per-CU LDS reservation           */
   int resolve_lds_kb;     /* resolver LDS reservation in KiB, 0 = by path (96 / 56)        */
@@ -274,6 +275,10 @@ typedef struct rc_tuning {
                              (0 never, 1 always, 2 for images of >= 32 Mpixel)              */
   int block_min;          /* regular carry segments of >= block_min entries are resolved by a
                              whole resolver workgroup (block windows), 0 = never             */
+  int pipe_inres;         /* frames in flight: phase C inside the resolver lanes (their idle
+                             waves shade ready batches) instead of on the pixel partition:
+                             0 never (default), 1 until the queue is drained, 2 until the
+                             lane's own resolver work is over (k_finish shades the rest)     */
 } rc_tuning;
 void rc_default_tuning(rc_tuning *t);
 int rc_set_tuning(const rc_tuning *t);

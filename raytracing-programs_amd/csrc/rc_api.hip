@@ -63,6 +63,7 @@ rc_tuning default_tuning() {
   t.copy_threads = 8;
   t.side_blocks = 0;
   t.comp_stream = 2;
+  t.pipe_inres = 0;
   t.block_min = 0;   // measured: 2048 slower in flight (5.46e9 vs 6.30e9) and at 8192^2
   return t;
 }
@@ -360,7 +361,7 @@ int rc_set_tuning(const rc_tuning* t) {
   if (!t) return -1;
   auto in = [](int v, int lo, int hi) { return v >= lo && v <= hi; };
   const bool ok =
-      in(t->side, 0, 3) && in(t->split_shade, 0, 1) && in(t->resolve_shared, 0, 1) &&
+      in(t->side, 0, 4) && in(t->split_shade, 0, 1) && in(t->resolve_shared, 0, 1) &&
       in(t->resolve_lds_kb, 0, 152) && (t->resolve_grid == 0 || in(t->resolve_grid, 8, 1 << 16)) &&
       in(t->team_blocks, -1, 256) && in(t->helpers, 0, rc::kDenseSlots) &&
       in(t->hand_run, 1, 1 << 30) && in(t->long_len, 64, 1 << 30) && in(t->wave_k, 1, 64) &&
@@ -370,7 +371,7 @@ int rc_set_tuning(const rc_tuning* t) {
       in(t->pipe_timing, 0, 1) && in(t->pipe_slotstreams, 0, 1) && in(t->overlap_d2h, 0, 1) &&
       in(t->staged_d2h, 0, 1) && in(t->prefault, 0, 1) && in(t->copy_threads, 1, 32) &&
       in(t->comp_stream, 0, 2) && in(t->side_blocks, 0, 1 << 16) &&
-      in(t->block_min, 0, 1 << 30) &&
+      in(t->block_min, 0, 1 << 30) && in(t->pipe_inres, 0, 2) &&
       !(t->split_shade && !t->side);
   if (!ok) {
     std::fprintf(stderr, "Error: rc_set_tuning: a field is out of range\n");
@@ -585,7 +586,7 @@ int ensure_parity(DevCtx& c, FrameBufs& b, int W, int H, rc::ParityWork& w, int 
   if (!w.side) w.split_shade = 0;   // split shading needs the side kernel
   // side 3: phase C inside the resolver (its waves shade ready batches once their own work is
   // done), a lone frame only
-  w.inres = (!piped && tu.side == 3) ? 1 : 0;
+  w.inres = (!piped && tu.side == 3) ? 1 : (!piped && tu.side == 4) ? 2 : 0;
   w.epoch = b.epoch;
   w.counters = (int*)b.counters.p;
   w.team = b.team.p;
@@ -1102,6 +1103,12 @@ int rc_frame_submit(const rc_scene* s, int W, int H, const rc_options* opt, uint
     std::fprintf(stderr, "Error: out of device memory for the parity workspace\n");
     return -1;
   }
+  // phase C in the resolver lanes (off by default): it pays where the pixel partition is the
+  // bound (reflection 2048^2 d4 8.2e9 -> 9.0e9 rays/s) and loses elsewhere (quadric 2048^2
+  // 3.27e9 -> 2.83e9, 4096^2 6.28e9 -> 5.36e9, 8192^2 8.6e9 -> 5.8e9, simple 1024^2 d6 3.16e9
+  // -> 2.98e9); mode 2 (no new batch once the lane's own work is over) does not change that
+  const int pin = tune().pipe_inres;
+  if (maxrec >= 3 && pin > 0) w.inres = pin;
   w.rstream = p.res[lane];
   w.pstream = first ? p.pix[p.fifo ? 0 : k] : nullptr;
   w.defer_c = p.fifo ? 1 : 0;

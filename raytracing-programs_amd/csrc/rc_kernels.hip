@@ -1235,7 +1235,8 @@ struct TeamState {
   // phase C's ready queue (lone frames with k_side): batches pushed as they complete, taken
   // by k_side's waves in that order (ready_range, phase_c_ready)
   int rq_prod, rq_cons;
-  int pad[26];
+  int helpers_out;   // helper workgroups past their hand-off loop (resolver_phase_c, mode 2)
+  int pad[25];
   TeamSlot slot[2][kTeamMax];
   DenseQueue dq;
 };
@@ -1502,11 +1503,24 @@ __device__ __forceinline__ void phase_c_ready(const Scene& sc, const Cam& cam, i
                                               const int* __restrict__ rq, uint8_t* __restrict__ out,
                                               uint32_t* __restrict__ patch, TeamState* ts,
                                               unsigned tag, int& zero,
-                                              unsigned* __restrict__ trace) {
+                                              unsigned* __restrict__ trace,
+                                              int stop_waves = 0, int stop_helpers = 0) {
   const int ndep = counters[2];
   const int nb = (ndep + 63) / 64;
   unsigned* tq = trace ? trace + 3 * (size_t)ndep + 5 * (size_t)counters[0] + 200000 : nullptr;
   for (;;) {
+    // stop_waves > 0 (phase C inside the resolver, mode 2): take no new item once the resolver's
+    // own work is over (every regular wave and helper done); k_finish shades the rest at full
+    // occupancy.  An item ticketed here is always shaded or left unclaimed for k_finish.
+    if (stop_waves > 0) {
+      int over = 0;
+      if ((threadIdx.x & 63) == 0)
+        over = __hip_atomic_load(&ts->dq.finished, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >=
+                   stop_waves &&
+               __hip_atomic_load(&ts->helpers_out, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >=
+                   stop_helpers;
+      if (__shfl(over, 0, 64)) break;
+    }
     const int k = wave_ticket(&ts->rq_cons);
     if (k >= nb) break;
     if (tq && (threadIdx.x & 63) == 0) tq[3 * k] = (unsigned)__builtin_amdgcn_s_memrealtime();
@@ -1558,10 +1572,12 @@ __device__ __forceinline__ void resolver_phase_c(const Scene& sc, const Cam& cam
                                               uint8_t* __restrict__ out,
                                               uint32_t* __restrict__ patch,
                                               unsigned long long* __restrict__ zcount,
-                                              TeamState* ts, unsigned tag) {
+                                              TeamState* ts, unsigned tag, int mode,
+                                              int helpers) {
   int zero = 0;
+  const int waves = ((int)gridDim.x - helpers) * (kResolveBlock / 64);
   phase_c_ready(sc, cam, W, maxrec, dep_pix, deprec, pcol, cin, counters, batch_state, rq, out,
-                patch, ts, tag, zero, nullptr);
+                patch, ts, tag, zero, nullptr, mode == 2 ? waves : 0, helpers);
   flush_events(zero, zcount);
 }
 
@@ -1891,8 +1907,12 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
     if (trace && lane == 0)   // debug trace: when each wave leaves
       trace[3 * (size_t)ndep + 5 * (size_t)nseg + 8 * 8192 + blockIdx.x * 4 + wave] =
           (unsigned)__builtin_amdgcn_s_memrealtime();
-    if (inres) resolver_phase_c(sc, cam, W, maxrec, dep_pix, deprec, wcarry, cin, counters,
-                                batch_state, rq, out, patch, zcount, ts, tag);
+    if (inres) {
+      if (threadIdx.x == 0)
+        __hip_atomic_fetch_add(&ts->helpers_out, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      resolver_phase_c(sc, cam, W, maxrec, dep_pix, deprec, wcarry, cin, counters, batch_state,
+                       rq, out, patch, zcount, ts, tag, inres, helpers);
+    }
     return;   // helpers take no regular segments
   }
 
@@ -2078,7 +2098,7 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
     trace[3 * (size_t)ndep + 5 * (size_t)nseg + 8 * 8192 + blockIdx.x * 4 + wave] =
         (unsigned)__builtin_amdgcn_s_memrealtime();
   if (inres) resolver_phase_c(sc, cam, W, maxrec, dep_pix, deprec, wcarry, cin, counters,
-                              batch_state, rq, out, patch, zcount, ts, tag);
+                              batch_state, rq, out, patch, zcount, ts, tag, inres, helpers);
 }
 template <bool kStage>
 __global__ void __launch_bounds__(kSideBlock) k_side(

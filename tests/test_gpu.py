@@ -60,6 +60,7 @@ def test_configs(key, scenes, table):
 SCHEDULES = {"no-side": dict(side=0), "side-always": dict(side=1), "side-by-size": dict(side=2),
              "in-resolver+no-dep-fast": dict(side=3, dep_fast=0),
              "in-resolver+no-helpers": dict(side=3, helpers=0),
+             "in-resolver-until-done": dict(side=4),
              "split-shade": dict(split_shade=1, side=1),
              "resolve-shared": dict(resolve_shared=1), "no-dep-fast": dict(dep_fast=0),
              "no-side+no-dep-fast": dict(side=0, dep_fast=0),
@@ -231,7 +232,9 @@ PIPES = {"default": {},
          "slot-streams": dict(pipe_slotstreams=1),
          "three-lanes": dict(pipe_resolvers=3, pipe_res_cus=144, pipe_slots=6),
          "one-lane-small-a": dict(pipe_resolvers=1, pipe_res_cus=32, pipe_timing=0),
-         "one-wg-per-cu": dict(resolve_lds_kb=96, team_blocks=24)}
+         "one-wg-per-cu": dict(resolve_lds_kb=96, team_blocks=24),
+         "phase-c-in-lanes": dict(pipe_inres=1),
+         "phase-c-in-lanes-until-done": dict(pipe_inres=2, pipe_slotstreams=1)}
 
 
 @pytest.mark.parametrize("pipe", list(PIPES))
