@@ -331,35 +331,71 @@ struct RowStats {
   long long wfirst;        // last writer before the row's first DEP pixel (-1: none)
 };
 
+// A row's class bytes reach LDS in 4 KiB chunks, 16 bytes per lane per load (a wave's 64
+// one-byte loads per chunk of 64 pixels were a chain of dependent round trips: k_row_stats
+// 39 us, k_row_compact 29 us at 4096^2); the ballot scans then read LDS.
+constexpr int kRowChunk = 4096;
+__device__ __forceinline__ void stage_row_chunk(const uint8_t* __restrict__ src, int n,
+                                                uint8_t* __restrict__ buf, int lane) {
+  if ((((size_t)src) & 15) == 0) {
+    for (int o = lane * 16; o < n; o += 64 * 16) {
+      if (o + 16 <= n) {
+        *(uint4*)(buf + o) = *(const uint4*)(src + o);
+      } else {
+        for (int i = o; i < n; ++i) buf[i] = src[i];
+      }
+    }
+  } else {
+    for (int i = lane; i < n; i += 64) buf[i] = src[i];
+  }
+}
+
+// zero (optional): the frame's counters and TeamState words, cleared here instead of by two
+// fill launches before this kernel (every workgroup clears a slice)
 __global__ void __launch_bounds__(256) k_row_stats(const uint8_t* __restrict__ cls, int W, int H,
-                                                   RowStats* __restrict__ rs) {
-  const int y = blockIdx.x * kRowWaves + (int)(threadIdx.x >> 6);
-  if (y >= H) return;
+                                                   RowStats* __restrict__ rs,
+                                                   int* __restrict__ counters,
+                                                   uint4* __restrict__ zero, int zero_words) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_row[kRowWaves][kRowChunk];
+  if (zero) {
+    const int g = blockIdx.x * 256 + threadIdx.x;
+    for (int i = g; i < zero_words; i += gridDim.x * 256) zero[i] = make_uint4(0, 0, 0, 0);
+    if (g < 16) counters[g] = 0;
+  }
+  const int wave = threadIdx.x >> 6;
+  const int y = blockIdx.x * kRowWaves + wave;
+  const bool on = y < H;
   const int lane = threadIdx.x & 63;
   const long long base = (long long)y * W;
   const unsigned long long lt = lanemask_lt();
   int nd = 0, ns = 0;
   long long lw = -1, ld = -1, wf = -1;
-  for (int x0 = 0; x0 < W; x0 += 64) {
-    const int x = x0 + lane;
-    const uint8_t c = x < W ? cls[base + x] : kClsIdent;
-    const unsigned long long md = __ballot(c == kClsDep), mw = __ballot(c == kClsWriter);
-    // a DEP lane (not the row's first DEP) starts a segment when a writer lies between it
-    // and the previous DEP: last writer before it > previous DEP before it
-    long long kw = (mw & lt) ? base + x0 + hi_bit(mw & lt) : lw;
-    long long pd = (md & lt) ? base + x0 + hi_bit(md & lt) : ld;
-    const bool st = c == kClsDep && pd >= 0 && kw > pd;
-    ns += __popcll(__ballot(st));
-    if (wf < 0 && ld < 0 && md) {   // first DEP of the row is in this chunk
-      const int f = __ffsll((long long)md) - 1;
-      const unsigned long long wb = mw & ((f ? (~0ull >> (64 - f)) : 0ull));
-      wf = wb ? base + x0 + hi_bit(wb) : lw;
+  for (int xc = 0; xc < W; xc += kRowChunk) {
+    const int n = W - xc < kRowChunk ? W - xc : kRowChunk;
+    if (on) stage_row_chunk(cls + base + xc, n, s_row[wave], lane);
+    __syncthreads();
+    for (int x0 = xc; on && x0 < xc + n; x0 += 64) {
+      const int x = x0 + lane;
+      const uint8_t c = x < W ? s_row[wave][x - xc] : kClsIdent;
+      const unsigned long long md = __ballot(c == kClsDep), mw = __ballot(c == kClsWriter);
+      // a DEP lane (not the row's first DEP) starts a segment when a writer lies between it
+      // and the previous DEP: last writer before it > previous DEP before it
+      long long kw = (mw & lt) ? base + x0 + hi_bit(mw & lt) : lw;
+      long long pd = (md & lt) ? base + x0 + hi_bit(md & lt) : ld;
+      const bool st = c == kClsDep && pd >= 0 && kw > pd;
+      ns += __popcll(__ballot(st));
+      if (wf < 0 && ld < 0 && md) {   // first DEP of the row is in this chunk
+        const int f = __ffsll((long long)md) - 1;
+        const unsigned long long wb = mw & ((f ? (~0ull >> (64 - f)) : 0ull));
+        wf = wb ? base + x0 + hi_bit(wb) : lw;
+      }
+      nd += __popcll(md);
+      if (mw) lw = base + x0 + hi_bit(mw);
+      if (md) ld = base + x0 + hi_bit(md);
     }
-    nd += __popcll(md);
-    if (mw) lw = base + x0 + hi_bit(mw);
-    if (md) ld = base + x0 + hi_bit(md);
+    __syncthreads();   // the chunk buffer is refilled
   }
-  if (lane == 0) rs[y] = RowStats{nd, ns, lw, ld, wf};
+  if (on && lane == 0) rs[y] = RowStats{nd, ns, lw, ld, wf};
 }
 
 // One workgroup of 1024: chunks of 1024 rows, wave-level inclusive scans + a carry.
@@ -460,37 +496,45 @@ __global__ void __launch_bounds__(256) k_row_compact(
     const int* __restrict__ row_soff, const long long* __restrict__ row_prevw,
     const long long* __restrict__ row_prevd, long long* __restrict__ dep_pix,
     int* __restrict__ seg_start, long long* __restrict__ seg_key) {
-  const int y = blockIdx.x * kRowWaves + (int)(threadIdx.x >> 6);
-  if (y >= H) return;
+  __shared__ __attribute__((aligned(16))) uint8_t s_row[kRowWaves][kRowChunk];
+  const int wave = threadIdx.x >> 6;
+  const int y = blockIdx.x * kRowWaves + wave;
+  const bool on = y < H;
   const int lane = threadIdx.x & 63;
   const long long base = (long long)y * W;
   const unsigned long long lt = lanemask_lt();
-  int idx0 = row_off[y], s0 = row_soff[y];
-  long long lw = row_prevw[y], ld = row_prevd[y];
-  for (int x0 = 0; x0 < W; x0 += 64) {
-    const int x = x0 + lane;
-    const uint8_t c = x < W ? cls[base + x] : kClsIdent;
-    const unsigned long long md = __ballot(c == kClsDep), mw = __ballot(c == kClsWriter);
-    if (md) {
-      const long long kw = (mw & lt) ? base + x0 + hi_bit(mw & lt) : lw;
-      const long long pd = (md & lt) ? base + x0 + hi_bit(md & lt) : ld;
-      const bool dep = c == kClsDep;
-      const bool st = dep && (pd < 0 || kw > pd);
-      const unsigned long long ms = __ballot(st);
-      if (dep) {
-        const int idx = idx0 + __popcll(md & lt);
-        dep_pix[idx] = base + x;
-        if (st) {
-          const int si = s0 + __popcll(ms & lt);
-          seg_start[si] = idx;
-          seg_key[si] = kw;
+  int idx0 = on ? row_off[y] : 0, s0 = on ? row_soff[y] : 0;
+  long long lw = on ? row_prevw[y] : -1, ld = on ? row_prevd[y] : -1;
+  for (int xc = 0; xc < W; xc += kRowChunk) {
+    const int n = W - xc < kRowChunk ? W - xc : kRowChunk;
+    if (on) stage_row_chunk(cls + base + xc, n, s_row[wave], lane);
+    __syncthreads();
+    for (int x0 = xc; on && x0 < xc + n; x0 += 64) {
+      const int x = x0 + lane;
+      const uint8_t c = x < W ? s_row[wave][x - xc] : kClsIdent;
+      const unsigned long long md = __ballot(c == kClsDep), mw = __ballot(c == kClsWriter);
+      if (md) {
+        const long long kw = (mw & lt) ? base + x0 + hi_bit(mw & lt) : lw;
+        const long long pd = (md & lt) ? base + x0 + hi_bit(md & lt) : ld;
+        const bool dep = c == kClsDep;
+        const bool st = dep && (pd < 0 || kw > pd);
+        const unsigned long long ms = __ballot(st);
+        if (dep) {
+          const int idx = idx0 + __popcll(md & lt);
+          dep_pix[idx] = base + x;
+          if (st) {
+            const int si = s0 + __popcll(ms & lt);
+            seg_start[si] = idx;
+            seg_key[si] = kw;
+          }
         }
+        idx0 += __popcll(md);
+        s0 += __popcll(ms);
+        ld = base + x0 + hi_bit(md);
       }
-      idx0 += __popcll(md);
-      s0 += __popcll(ms);
-      ld = base + x0 + hi_bit(md);
+      if (mw) lw = base + x0 + hi_bit(mw);
     }
-    if (mw) lw = base + x0 + hi_bit(mw);
+    __syncthreads();   // the chunk buffer is refilled
   }
 }
 
@@ -1240,6 +1284,8 @@ struct TeamState {
   TeamSlot slot[2][kTeamMax];
   DenseQueue dq;
 };
+
+static_assert(sizeof(TeamState) % 16 == 0, "k_row_stats clears TeamState in 16-byte words");
 
 constexpr unsigned long long kSpinLimit = 500000000ull;   // 5 s of the 100 MHz clock
 constexpr unsigned long long kSpinPoll = 100000ull;       // check the error word after 1 ms
@@ -2537,11 +2583,12 @@ hipError_t launch_parity(const LaunchScene& s, int W, int H, int maxrec, uint8_t
     (void)hipStreamWaitEvent(w.cstream, w.adone, 0);
     stream = w.cstream;
   }
-  (void)hipMemsetAsync(w.counters, 0, 16 * sizeof(int), stream);   // nseg, head, ndep, ...
-  (void)hipMemsetAsync(w.team, 0, sizeof(TeamState), stream);     // error + round tags
+  // k_row_stats clears the counters (nseg, head, ndep, ...) and the TeamState (error word,
+  // round tags, queues) before anything reads them
   const int row_blocks = (H + kRowWaves - 1) / kRowWaves;
   hipLaunchKernelGGL(k_row_stats, dim3(row_blocks), dim3(256), 0, stream, w.cls, W, H,
-                     (RowStats*)w.row_stats);
+                     (RowStats*)w.row_stats, w.counters, (uint4*)w.team,
+                     (int)(sizeof(TeamState) / sizeof(uint4)));
   hipLaunchKernelGGL(k_row_scan, dim3(1), dim3(1024), 0, stream, H, (const RowStats*)w.row_stats,
                      w.row_off, w.row_soff, w.row_prevw, w.row_prevd, w.counters);
   hipLaunchKernelGGL(k_row_compact, dim3(row_blocks), dim3(256), 0, stream, w.cls, W, H,
@@ -2700,7 +2747,7 @@ hipError_t launch_shard_local(const LaunchScene& s, int W, int H, int row0, int 
                      (DepRec*)w.deprec, zcount);
   const int row_blocks = (nrows + kRowWaves - 1) / kRowWaves;
   hipLaunchKernelGGL(k_row_stats, dim3(row_blocks), dim3(256), 0, stream, w.cls, W, nrows,
-                     (RowStats*)w.row_stats);
+                     (RowStats*)w.row_stats, nullptr, nullptr, 0);
   hipLaunchKernelGGL(k_row_scan, dim3(1), dim3(1024), 0, stream, nrows,
                      (const RowStats*)w.row_stats, w.row_off, w.row_soff, w.row_prevw,
                      w.row_prevd, w.counters);

@@ -13,6 +13,6 @@ for t in ${PIPE:-}; do
   echo "bench $t"; timeout -k 10 200 python -u bench.py --timed-only --steps 30 --warmup 3 --tune ${t//,/ --tune } | python3 -c "import json,sys; l=json.loads(sys.stdin.read().strip().splitlines()[-1]); print(l['value'], l['ms_per_step'], l['verified']['frames'], l['roofline']['kernel_ms'])" || exit 1
 done
 for t in ${TRACE:-}; do
-  RC_HIP_LIB=libraycast_hip_stamps.so RC_RESOLVE_TRACE=gpurun_out/trace_$t.txt TUNE=$t timeout -k 10 120 python -u scripts/trace_run.py && python3 scripts/seg_trace.py gpurun_out/trace_$t.txt | grep -v "^  " || exit 1
+  RC_HIP_LIB=${STAMPLIB:-libraycast_hip_stamps2.so} RC_RESOLVE_TRACE=gpurun_out/trace_$t.txt TUNE=$t timeout -k 10 120 python -u scripts/trace_run.py && python3 scripts/seg_trace.py gpurun_out/trace_$t.txt | grep -v "^  " || exit 1
   tail -8 gpurun_out/trace_$t.txt.cyc
 done
