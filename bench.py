@@ -73,7 +73,9 @@ def load_pkg():
 
 # rocprofv3 --pmc summaries of this exact configuration from HEAD (scripts/pmc_valu.sh,
 # scripts/pmc_fast.sh -> scripts/pmc_summary.py): per-kernel counter means per launch.
-PMC_PROFILES = {("quadric", 4096, 6, "parity"): "profiles/r02g_pmc_lone_4096.json",
+PMC_PROFILES = {("quadric", 4096, 6, "parity"): "profiles/r03b_pmc_lone_4096.json",
+                ("reflection", 2048, 4, "parity"): "profiles/r03b_pmc_lone_c3.json",
+                ("quadric", 8192, 6, "parity"): "profiles/r03b_pmc_lone_c5.json",
                 ("quadric", 4096, 6, "fast"): "profiles/r02c_pmc_fast_4096.json"}
 
 
@@ -649,10 +651,13 @@ def main():
         ms = (time.perf_counter() - ts) * 1e3 / reps
         st = group.stats()
         leg = {"value": round(W * H / (ms * 1e-3), 1), "unit": "rays/s", "ms": round(ms, 4),
-               "note": f"one {W}x{H} image row-sharded over {world} GPUs (rc_render_sharded: "
-                       "phase A on every rank, DEP entries gathered to rank 0 over RCCL, "
-                       "serial carry resolver there, carry-ins back, phase C on every rank, "
-                       "row blocks gathered); strong scaling, capped by the resolver",
+               "note": (f"one {W}x{H} image row-sharded over {world} GPUs (rc_render_sharded: "
+                        "phase A on every rank, DEP entries gathered to rank 0 over RCCL, "
+                        "serial carry resolver there, carry-ins back, phase C on every rank, "
+                        "row blocks gathered); strong scaling, capped by the resolver")
+                       if world > 1 else
+                       (f"one {W}x{H} image through rc_render_sharded with one rank: nothing "
+                        "to exchange, the rank renders it as a lone frame"),
                "stats": {k: (round(v, 4) if isinstance(v, float) else v)
                          for k, v in (st or {}).items()}}
         if rank == 0:

@@ -545,6 +545,7 @@ int ensure_parity(DevCtx& c, FrameBufs& b, int W, int H, rc::ParityWork& w, int 
   w.batch_state = (int*)b.batch_state.p;   // claim words, then completion counts, then queue
   w.batch_cnt = w.batch_state + (P / 64 + 2);
   w.batch_rq = w.batch_state + 2 * (P / 64 + 2);
+  w.batch_ints = (int)(3 * (P / 64 + 2));
   w.side = nullptr;
   w.rstream = nullptr;
   w.pstream = nullptr;
@@ -648,7 +649,7 @@ int enqueue_render_ws(DevCtx& c, const rc_scene* s, int W, int H, int row0, int 
 // one-frame workspace c.fb: after the previous render that used it, whatever its stream.
 int enqueue_render(DevCtx& c, const rc_scene* s, int W, int H, int row0, int row_step, int nrows,
                    const rc_options* opt, uint8_t* d_out, hipStream_t stream, bool timed,
-                   uint32_t* patch = nullptr, hipEvent_t** evset = nullptr) {
+                   uint32_t* patch, hipEvent_t** evset) {
   if (c.ws_valid && c.ws_stream != stream) HIP_TRY(hipStreamWaitEvent(stream, c.ws_ev, 0));
   const int rc = enqueue_render_ws(c, s, W, H, row0, row_step, nrows, opt, d_out, stream, timed,
                                    patch, evset);

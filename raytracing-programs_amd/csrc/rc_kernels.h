@@ -72,6 +72,7 @@ struct ParityWork {
   int defer_c;              // pipelined: launch_parity stops after the resolver; phase C is
                             // enqueued later by launch_phase_c (after rdone)
   int inject;               // test aid: the resolver raises its error word (code 4) at start
+  int batch_ints;           // ints from batch_state on (claims, counts, queue), cleared by k_row_stats
   int inres;                // phase C inside the resolver: its waves shade ready batches once
                             // their own work is done (rc_tuning.side 3)
   int block_min;            // regular segments of >= block_min entries get a whole workgroup

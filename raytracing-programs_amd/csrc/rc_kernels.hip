@@ -355,11 +355,13 @@ __device__ __forceinline__ void stage_row_chunk(const uint8_t* __restrict__ src,
 __global__ void __launch_bounds__(256) k_row_stats(const uint8_t* __restrict__ cls, int W, int H,
                                                    RowStats* __restrict__ rs,
                                                    int* __restrict__ counters,
-                                                   uint4* __restrict__ zero, int zero_words) {
+                                                   uint4* __restrict__ zero, int zero_words,
+                                                   int* __restrict__ zero2, int zero2_ints) {
   __shared__ __attribute__((aligned(16))) uint8_t s_row[kRowWaves][kRowChunk];
   if (zero) {
     const int g = blockIdx.x * 256 + threadIdx.x;
     for (int i = g; i < zero_words; i += gridDim.x * 256) zero[i] = make_uint4(0, 0, 0, 0);
+    for (int i = g; i < zero2_ints; i += gridDim.x * 256) zero2[i] = 0;
     if (g < 16) counters[g] = 0;
   }
   const int wave = threadIdx.x >> 6;
@@ -947,14 +949,16 @@ __global__ void __launch_bounds__(1024) k_seg_order(const int* __restrict__ seg_
                                                      int* __restrict__ batch_state,
                                                      int* __restrict__ batch_cnt,
                                                      int* __restrict__ batch_rq,
-                                                     int block_min) {
+                                                     int block_min, int zero_batches) {
   const int nseg = counters[0], ndep = counters[2];
   // phase C's per-batch claim words (64 DEP entries per batch), completion counts and ready
-  // queue, zeroed for this frame
-  for (int b = threadIdx.x; b < (ndep + 63) / 64; b += blockDim.x) {
-    batch_state[b] = 0;
-    batch_cnt[b] = 0;
-    batch_rq[b] = 0;
+  // queue are zeroed for this frame: by k_row_stats (launch_parity, batch_ints > 0), else here
+  if (zero_batches) {
+    for (int b = threadIdx.x; b < (ndep + 63) / 64; b += blockDim.x) {
+      batch_state[b] = 0;
+      batch_cnt[b] = 0;
+      batch_rq[b] = 0;
+    }
   }
   if (nseg > kSegOrderMax) {
     if (threadIdx.x == 0) {
@@ -2588,14 +2592,15 @@ hipError_t launch_parity(const LaunchScene& s, int W, int H, int maxrec, uint8_t
   const int row_blocks = (H + kRowWaves - 1) / kRowWaves;
   hipLaunchKernelGGL(k_row_stats, dim3(row_blocks), dim3(256), 0, stream, w.cls, W, H,
                      (RowStats*)w.row_stats, w.counters, (uint4*)w.team,
-                     (int)(sizeof(TeamState) / sizeof(uint4)));
+                     (int)(sizeof(TeamState) / sizeof(uint4)), w.batch_state, w.batch_ints);
   hipLaunchKernelGGL(k_row_scan, dim3(1), dim3(1024), 0, stream, H, (const RowStats*)w.row_stats,
                      w.row_off, w.row_soff, w.row_prevw, w.row_prevd, w.counters);
   hipLaunchKernelGGL(k_row_compact, dim3(row_blocks), dim3(256), 0, stream, w.cls, W, H,
                      w.row_off, w.row_soff, w.row_prevw, w.row_prevd, w.dep_pix, w.seg_start,
                      w.seg_key);
   hipLaunchKernelGGL(k_seg_order, dim3(1), dim3(1024), 0, stream, w.seg_start, w.counters,
-                     w.seg_order, w.batch_state, w.batch_cnt, w.batch_rq, w.block_min);
+                     w.seg_order, w.batch_state, w.batch_cnt, w.batch_rq, w.block_min,
+                     w.batch_ints > 0 ? 0 : 1);
   // resolve_lds > 80 KiB keeps one resolver block (4 waves, one per SIMD) per CU: the chain
   // steps are latency-bound, so a resolver wave should not share its SIMD
   if (ev) (void)hipEventRecord(ev[1], stream);
@@ -2747,7 +2752,7 @@ hipError_t launch_shard_local(const LaunchScene& s, int W, int H, int row0, int 
                      (DepRec*)w.deprec, zcount);
   const int row_blocks = (nrows + kRowWaves - 1) / kRowWaves;
   hipLaunchKernelGGL(k_row_stats, dim3(row_blocks), dim3(256), 0, stream, w.cls, W, nrows,
-                     (RowStats*)w.row_stats, nullptr, nullptr, 0);
+                     (RowStats*)w.row_stats, nullptr, nullptr, 0, nullptr, 0);
   hipLaunchKernelGGL(k_row_scan, dim3(1), dim3(1024), 0, stream, nrows,
                      (const RowStats*)w.row_stats, w.row_off, w.row_soff, w.row_prevw,
                      w.row_prevd, w.counters);
@@ -2779,7 +2784,7 @@ hipError_t launch_shard_resolve(const LaunchScene& s, int W, int H, int G, int r
                      w.row_prevw, w.row_prevd, (DepRec*)w.deprec, w.dep_pix, w.seg_start,
                      w.seg_key, w.wcarry, bound);
   hipLaunchKernelGGL(k_seg_order, dim3(1), dim3(1024), 0, stream, w.seg_start, w.counters,
-                     w.seg_order, w.batch_state, w.batch_cnt, w.batch_rq, w.block_min);
+                     w.seg_order, w.batch_state, w.batch_cnt, w.batch_rq, w.block_min, 1);
   if (ev) (void)hipEventRecord(ev[0], stream);
   auto kres = s.n <= kLdsShapes ? k_resolve<true> : k_resolve<false>;
   hipLaunchKernelGGL(kres, dim3(w.resolve_blocks), dim3(kResolveBlock), w.resolve_lds, stream,

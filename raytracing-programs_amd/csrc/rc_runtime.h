@@ -185,6 +185,13 @@ int ensure_parity(DevCtx& c, FrameBufs& b, int W, int H, rc::ParityWork& w, int 
                   int piped_lane = -1);
 int report_spin_error(const FrameBufs& b, const char* where);
 double event_ms(hipEvent_t a, hipEvent_t b);
+// One render of rows row0 + k*row_step into d_out on `stream` through the device's one-frame
+// workspace (rc_render_device's path; the caller holds c.mu).  timed: phase events c.ev[0].
+int enqueue_render(DevCtx& c, const rc_scene* s, int W, int H, int row0, int row_step, int nrows,
+                   const rc_options* opt, uint8_t* d_out, hipStream_t stream, bool timed,
+                   uint32_t* patch = nullptr, hipEvent_t** evset = nullptr);
+int check_spin_error(FrameBufs& b, const rc_options* opt);
+void fill_device_timing(DevCtx& c, const rc_options* opt, rc_timing* t);
 // rc_shard.hip: rc_render's multi-GPU path (a cached in-process group over devices
 // first..first+n-1); *d_image = the root's de-interleaved image.  The caller holds no lock.
 int render_local_group(int first, int n, const rc_scene* s, int W, int H, const rc_options* opt,

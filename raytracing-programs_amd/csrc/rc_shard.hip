@@ -278,6 +278,58 @@ double ms_since(std::chrono::steady_clock::time_point t0) {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
 
+// A group of one rank has nothing to exchange: the rank renders the whole image as a lone
+// frame (rc_render_device's path, phase C inside the resolver) into d_image on its stream.
+// The sharded machinery (wire records, gathers, the root's resolver on gathered entries,
+// phase C after it) cost 1.2 ms more at 4096^2 (profiles/r03b_bench_force_group.log).
+int render_one_rank(rc_group& g, const rc_scene* s, int W, int H, const rc_options* opt,
+                    uint8_t* d_image, rc_timing* timing,
+                    std::chrono::steady_clock::time_point t0) {
+  Rank& r = *g.root;
+  HIP_TRY(hipSetDevice(r.device));
+  if (!d_image) {
+    if (r.image.ensure((size_t)H * W * 3)) return -1;
+    d_image = (uint8_t*)r.image.p;
+  }
+  DevCtx& c = *r.c;
+  if (c.lone_log.poll() > 0) {   // an earlier lone frame of this workspace failed
+    c.lone_log.take(nullptr, nullptr);
+    return -1;
+  }
+  // the scene upload and the phase events live on the ctx stream: the rank's stream here
+  hipStream_t saved = c.stream;
+  c.stream = r.stream;
+  const int rc = enqueue_render(c, s, W, H, 0, 1, H, opt, d_image, r.stream, true);
+  c.stream = saved;
+  if (rc) return -1;
+  HIP_TRY(hipStreamSynchronize(r.stream));
+  if (c.lone_log.poll() > 0) {
+    c.lone_log.take(nullptr, nullptr);
+    return -1;
+  }
+  if (check_spin_error(c.fb, opt)) return -1;
+  rc_timing t{};
+  fill_device_timing(c, opt, &t);
+  rc_shard_stats& st = g.last;
+  std::memset(&st, 0, sizeof st);
+  st.total_ms = ms_since(t0);
+  st.ranks = 1;
+  st.device_ms = t.kernel_ms;
+  st.resolve_ms = t.resolve_ms;
+  st.dep_pixels = t.dep_pixels;
+  st.zero_normalize = t.zero_normalize;
+  st.image_bytes = (long long)H * W * 3;
+  if (timing) {
+    std::memset(timing, 0, sizeof *timing);
+    timing->total_ms = st.total_ms;
+    timing->kernel_ms = st.device_ms;
+    timing->resolve_ms = st.resolve_ms;
+    timing->dep_pixels = st.dep_pixels;
+    timing->zero_normalize = st.zero_normalize;
+  }
+  return 0;
+}
+
 // The whole sharded render; the caller holds every driven device's lock.
 int render_sharded(rc_group& g, const rc_scene* s, int W, int H, const rc_options* opt,
                    uint8_t* d_image, rc_timing* timing) {
@@ -289,6 +341,7 @@ int render_sharded(rc_group& g, const rc_scene* s, int W, int H, const rc_option
   const size_t row_bytes = (size_t)W * 3;
   const size_t block_bytes = (size_t)rmax * row_bytes;
   Rank* root = g.root;
+  if (G == 1 && root) return render_one_rank(g, s, W, H, opt, d_image, timing, t0);
   if (root) {
     HIP_TRY(hipSetDevice(root->device));
     if (!d_image) {

@@ -23,6 +23,7 @@ run bench_c3p 120 python -u bench.py --scene reflection --size 2048 --depth 4 --
 run bench_c5p 200 python -u bench.py --size 8192 --steps 20 --no-cpu-baseline
 run bench_s1024 120 python -u bench.py --scene simple --size 1024 --no-cpu-baseline
 run bench_fast 120 python -u bench.py --mode fast --no-cpu-baseline
+run bench_force_group 200 python -u bench.py --force-group --no-cpu-baseline
 run rocprof_stats 200 rocprofv3 --kernel-trace --stats --output-format csv -d $out/stats -o stats -- python -u bench.py --timed-only --steps 20 --warmup 3
 run pmc_fetch 90 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $out/fetch -o fetch -- python -u bench.py --timed-only --steps 3 --warmup 1
 run pmc_write 90 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $out/write -o write -- python -u bench.py --timed-only --steps 3 --warmup 1
