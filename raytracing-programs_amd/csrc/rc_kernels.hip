@@ -1324,26 +1324,30 @@ __device__ __forceinline__ void ready_range(int* __restrict__ cnt, int* __restri
   if (!cnt || j0 >= j1) return;
   const int lane = threadIdx.x & 63;
   const int b0 = j0 >> 6, b1 = (j1 - 1) >> 6;
-  for (int bb = b0; bb <= b1; bb += 64) {
-    const int b = bb + lane;
-    bool done = false;
-    if (b <= b1) {
-      const int lo = j0 > b * 64 ? j0 : b * 64;
-      const int hi = j1 < b * 64 + 64 ? j1 : b * 64 + 64;
-      const int size = (ndep < b * 64 + 64 ? ndep : b * 64 + 64) - b * 64;
-      const int add = hi - lo;
-      done = add == size || atomicAdd(&cnt[b], add) + add == size;
-    }
-    const unsigned long long m = __ballot(done);
-    if (m) {
-      int k0 = 0;
-      if (lane == 0) k0 = atomicAdd(&ts->rq_prod, __popcll(m));
-      k0 = __shfl(k0, 0, 64);
-      if (done)
-        __hip_atomic_store(&rq[k0 + __popcll(m & lanemask_lt())], b + 1, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    }
+  // [j0, j1) is contiguous: only its first and last batch can be partial, so at most two
+  // credit atomics (lanes 0 and 1, in flight together) and one queue reservation for every
+  // completed batch — a team SCAN round completes ~512 batches, which took eight dependent
+  // reservations when they were made per 64 batches
+  int r = 1;
+  if (lane < 2 && (lane == 0 || b1 != b0)) {
+    const int b = lane == 0 ? b0 : b1;
+    const int lo = j0 > b * 64 ? j0 : b * 64;
+    const int hi = j1 < b * 64 + 64 ? j1 : b * 64 + 64;
+    const int size = (ndep < b * 64 + 64 ? ndep : b * 64 + 64) - b * 64;
+    const int add = hi - lo;
+    r = (add == size || atomicAdd(&cnt[b], add) + add == size) ? 1 : 0;
   }
+  const bool d0 = __shfl(r, 0, 64) != 0;
+  const bool d1 = b1 != b0 ? __shfl(r, 1, 64) != 0 : d0;
+  const int first = d0 ? b0 : b0 + 1;
+  const int last = b1 != b0 ? (d1 ? b1 : b1 - 1) : (d0 ? b0 : b0 - 1);
+  const int n = last - first + 1;
+  if (n <= 0) return;
+  int k0 = 0;
+  if (lane == 0) k0 = atomicAdd(&ts->rq_prod, n);
+  k0 = __shfl(k0, 0, 64);
+  for (int i = lane; i < n; i += 64)
+    __hip_atomic_store(&rq[k0 + i], first + i + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __device__ __forceinline__ void team_publish(TeamState* ts, int round, unsigned pos, V3 c) {
@@ -1715,6 +1719,16 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
       V3 c = seg_init_carry(seg_key, wcarry, s);
       int j = start;
       bool resolve = false;
+      // the next SCAN round's record, loaded one round ahead (most SCAN rounds cross a clean
+      // stretch, so the next window is j + window): its two dependent loads then overlap this
+      // round's evaluation instead of following the round's hand-off and carry-in stores
+      DepRec pre;
+      int pre_idx = -1;
+      // the previous round's entries, credited to phase C's ready queue by the team's last
+      // block while it waits for the next round's hand-off (its latency then overlaps the
+      // wait instead of delaying the block's own round)
+      int pend0 = 0, pend1 = 0;
+      const bool crediter = (int)blockIdx.x == T - 1 && wave == 0;
       while (j < end) {
         ++round;
         ++rounds_here;
@@ -1729,9 +1743,13 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
           const bool valid = idx < end;
           V3 o = c;
           bool h = false;
+          DepRec r;
+          if (valid) r = pre_idx == idx ? pre : rec_at(deprec, dep_pix, idx);
+          pre_idx = idx + window;
+          if (pre_idx < end) pre = rec_at(deprec, dep_pix, pre_idx);
           if (valid) {
             int zero = 0;
-            o = carry_path(sc, rec_at(deprec, dep_pix, idx), maxrec, c, zero, h);
+            o = carry_path(sc, r, maxrec, c, zero, h);
           }
           const unsigned long long m = __ballot(valid && !same_bits(o, c));
           const int k = m ? __ffsll((long long)m) - 1 : -1;
@@ -1749,6 +1767,10 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
             const bool hit = s_pos[w] != 0x7fffffff;
             team_publish(ts, round, (unsigned)s_pos[w],
                          hit ? v3(s_o[w][0], s_o[w][1], s_o[w][2]) : v3(0.0f, 0.0f, 0.0f));
+          }
+          if (crediter) {
+            ready_range(rq_cnt, rq, ts, ndep, pend0, pend1);
+            pend0 = pend1 = 0;
           }
           // every thread t < T collects slot t; block-wide minimum position
           unsigned upos = 0x7fffffffu;
@@ -1814,6 +1836,10 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
             }
             if (threadIdx.x == 0) team_publish(ts, round, (unsigned)j, c);
           }
+          if (crediter && T > 1) {
+            ready_range(rq_cnt, rq, ts, ndep, pend0, pend1);
+            pend0 = pend1 = 0;
+          }
           if (threadIdx.x == 0) {
             unsigned upos = 0;
             V3 oc;
@@ -1830,10 +1856,12 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
           resolve = false;
           __syncthreads();
         }
-        // the round's entries [j_round, j) are published: the team's last block credits them
-        // to phase C's ready queue (off the leader's chain)
-        if ((int)blockIdx.x == T - 1 && wave == 0)
-          ready_range(rq_cnt, rq, ts, ndep, j_round, j < end ? j : end);
+        // the round's entries [j_round, j) are published: credited during the next round's
+        // wait (pend), or below when the segment ends
+        if (crediter) {
+          pend0 = j_round;
+          pend1 = j < end ? j : end;
+        }
         // debug trace: per-round team log after the per-segment records and stamps
         if (trace && blockIdx.x == 0 && wave == 0 && lane == 0 && round < 8192) {
           unsigned* tl = trace + 3 * (size_t)ndep + 4 * (size_t)nseg + 8 * (size_t)round;
@@ -1853,6 +1881,7 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
 #endif
         }
       }
+      if (crediter) ready_range(rq_cnt, rq, ts, ndep, pend0, pend1);   // the last round's
       if (trace && blockIdx.x == 0 && threadIdx.x == 0) {
         trace[3 * s] = (unsigned)(__builtin_amdgcn_s_memrealtime() - t_seg);
         trace[3 * s + 1] = (unsigned)rounds_here | 0x80000000u;

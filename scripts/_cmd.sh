@@ -1,5 +1,9 @@
 mkdir -p gpurun_out
-SIZE=4096 CHECK=1 TAG=lone4096 REPS=10 timeout -k 10 120 python -u scripts/lone.py || exit 1
-timeout -k 10 300 python -u bench.py --force-group --no-cpu-baseline > gpurun_out/fg.log 2>&1 || { tail -5 gpurun_out/fg.log; exit 1; }
-tail -1 gpurun_out/fg.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'], d['single_frame']['ms'], json.dumps(d['sharded_single_image'])[:400])"
-timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests -m gpu > gpurun_out/tg.log 2>&1; rc=$?; tail -3 gpurun_out/tg.log; exit $rc
+for t in block_min=0 block_min=3000; do
+  SIZE=4096 CHECK=1 TAG="lone4096 $t" TUNE=$t REPS=10 timeout -k 10 120 python -u scripts/lone.py || exit 1
+done
+RC_HIP_LIB=libraycast_hip_stamps2.so RC_RESOLVE_TRACE=gpurun_out/trace_pf.txt TUNE=block_min=3000 timeout -k 10 120 python -u scripts/trace_run.py && python3 scripts/seg_trace.py gpurun_out/trace_pf.txt > gpurun_out/seg_pf.txt || exit 1
+head -6 gpurun_out/seg_pf.txt
+awk '$2==0 {s+=$5; n++} $2==1 {r+=$5; m++} END {print "scan", n, s, "resolve", m, r}' gpurun_out/trace_pf.txt.team
+timeout -k 10 200 python -u bench.py --timed-only --no-cpu-baseline --steps 30 --warmup 3 > gpurun_out/b.log 2>&1 || { tail -5 gpurun_out/b.log; exit 1; }
+tail -1 gpurun_out/b.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'], d.get('verified')['frames'])"
