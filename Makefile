@@ -93,6 +93,11 @@ $(OBJ)/coalesced_kernels.o: $(SRC)/rc_kernels.hip $(HIP_HDRS)
 	$(HIPCC) $(HIPFLAGS) -DRC_TILE_W=32 -DRC_TILE_STAGE=1 -c $< -o $@
 $(OBJ)/t16_kernels.o: $(SRC)/rc_kernels.hip $(HIP_HDRS)
 	$(HIPCC) $(HIPFLAGS) -DRC_TILE_W=16 -DRC_TILE_STAGE=1 -c $< -o $@
+# occupancy variants of the pixel kernels (RC_PHASE_A_WAVES waves per SIMD)
+$(OBJ)/pa5_kernels.o: $(SRC)/rc_kernels.hip $(HIP_HDRS)
+	$(HIPCC) $(HIPFLAGS) -DRC_PHASE_A_WAVES=5 -c $< -o $@
+$(OBJ)/pa6_kernels.o: $(SRC)/rc_kernels.hip $(HIP_HDRS)
+	$(HIPCC) $(HIPFLAGS) -DRC_PHASE_A_WAVES=6 -c $< -o $@
 $(LIB)/libraycast_hip_%.so: $(OBJ)/%_kernels.o $(OBJ)/rc_api.o $(OBJ)/rc_shard.o $(OBJ)/rc_scene.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -o $@ $(HIPLIBS)
 

@@ -274,7 +274,8 @@ typedef struct rc_tuning {
   int comp_stream;        /* frames in flight: compaction on an unmasked top-priority stream
                              (0 never, 1 always, 2 for images of >= 32 Mpixel)              */
   int block_min;          /* regular carry segments of >= block_min entries are resolved by a
-                             whole resolver workgroup (block windows), 0 = never             */
+                             whole resolver workgroup (block windows) when the grid has a
+                             workgroup for each of them, 0 = never (default 3000)            */
   int pipe_inres;         /* frames in flight: phase C inside the resolver lanes (their idle
                              waves shade ready batches) instead of on the pixel partition:
                              0 never (default), 1 until the queue is drained, 2 until the

@@ -64,7 +64,11 @@ rc_tuning default_tuning() {
   t.side_blocks = 0;
   t.comp_stream = 2;
   t.pipe_inres = 0;
-  t.block_min = 0;   // measured: 2048 slower in flight (5.46e9 vs 6.30e9) and at 8192^2
+  // regular segments of >= 3000 entries on whole workgroups when there are workgroups for all
+  // of them (k_seg_order): lone quadric 4096^2 5.19 -> 5.06 ms (its ~100 3856-entry segments
+  // 4.4 -> 2.5 ms, under the team segment); 8192^2 and pipeline lanes have more such segments
+  // than workgroups and keep one wave per segment
+  t.block_min = 3000;
   return t;
 }
 rc_tuning g_tune = default_tuning();

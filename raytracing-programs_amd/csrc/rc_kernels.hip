@@ -949,7 +949,8 @@ __global__ void __launch_bounds__(1024) k_seg_order(const int* __restrict__ seg_
                                                      int* __restrict__ batch_state,
                                                      int* __restrict__ batch_cnt,
                                                      int* __restrict__ batch_rq,
-                                                     int block_min, int zero_batches) {
+                                                     int block_min, int block_cap,
+                                                     int zero_batches) {
   const int nseg = counters[0], ndep = counters[2];
   // phase C's per-batch claim words (64 DEP entries per batch), completion counts and ready
   // queue are zeroed for this frame: by k_row_stats (launch_parity, batch_ints > 0), else here
@@ -992,6 +993,12 @@ __global__ void __launch_bounds__(1024) k_seg_order(const int* __restrict__ seg_
       acc += hist[b];
       if (block_min > 0 && 255 - b >= bmin) nlong = acc;
     }
+    // whole workgroups for the long regular segments only when the regular workgroups can
+    // take them in at most two turns: a workgroup resolves a 3 856-entry segment in ~0.55x a
+    // lone wave's time at worst and most of them much faster (quadric 4096^2: 154 such
+    // segments on 120 workgroups, all done by 2.5 ms); with more the turns queue up and it
+    // loses (8192^2 lone 12.9 -> 14.4 ms, frames in flight at 4096^2 5.5e9 vs 6.3e9 rays/s)
+    if (nlong > 2 * block_cap) nlong = 0;
     counters[14] = nlong;
     counters[15] = nlong;
   }
@@ -1635,8 +1642,10 @@ __device__ __forceinline__ void resolver_phase_c(const Scene& sc, const Cam& cam
   flush_events(zero, zcount);
 }
 
+// amdgpu_waves_per_eu(2): a pipeline lane places two resolver workgroups per CU (one wave per
+// SIMD each), so the kernel must stay within 256 registers (VGPRs + AGPRs) per wave
 template <bool kLds>
-__global__ void __launch_bounds__(kResolveBlock) k_resolve(
+__global__ void __launch_bounds__(kResolveBlock) __attribute__((amdgpu_waves_per_eu(2))) k_resolve(
     Scene sc, int maxrec, const DepRec* __restrict__ deprec,
     const long long* __restrict__ dep_pix, const long long* __restrict__ seg_key,
     const float4* __restrict__ wcarry,
@@ -1719,11 +1728,10 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
       V3 c = seg_init_carry(seg_key, wcarry, s);
       int j = start;
       bool resolve = false;
-      // the next SCAN round's record, loaded one round ahead (most SCAN rounds cross a clean
-      // stretch, so the next window is j + window): its two dependent loads then overlap this
-      // round's evaluation instead of following the round's hand-off and carry-in stores
-      DepRec pre;
-      int pre_idx = -1;
+      // SCAN width: sub-windows of `window` entries per round, doubled after every clean
+      // round up to 4 (a clean stretch then costs one hand-off per 4 windows), back to 1 after
+      // a changer; the same on every team block (it follows the agreed positions)
+      int width = 1;
       // the previous round's entries, credited to phase C's ready queue by the team's last
       // block while it waits for the next round's hand-off (its latency then overlaps the
       // wait instead of delaying the block's own round)
@@ -1738,26 +1746,45 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
         const bool was_resolve = resolve;
         if (!resolve) {
           // ---------------------------------------------------------------- SCAN
-          const int base = j + ((int)blockIdx.x * 4 + wave) * 64;
-          const int idx = base + lane;
-          const bool valid = idx < end;
-          V3 o = c;
-          bool h = false;
-          DepRec r;
-          if (valid) r = pre_idx == idx ? pre : rec_at(deprec, dep_pix, idx);
-          pre_idx = idx + window;
-          if (pre_idx < end) pre = rec_at(deprec, dep_pix, pre_idx);
-          if (valid) {
-            int zero = 0;
-            o = carry_path(sc, r, maxrec, c, zero, h);
+          // sub-window q: entries j + q*window + (block*4 + wave)*64 + lane; a wave stops at
+          // its first changer (everything after it in scan order is after it in the window)
+          const int slice = ((int)blockIdx.x * 4 + wave) * 64;
+          unsigned long long hmq[4] = {0, 0, 0, 0};
+          // one record ahead (two live, not four: the lanes' two resolver workgroups per CU
+          // need the kernel within 256 registers)
+          DepRec cur;
+          if (j + slice + lane < end) cur = rec_at(deprec, dep_pix, j + slice + lane);
+          int wpos = 0x7fffffff;
+          V3 wo = c;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            if (q < width && wpos == 0x7fffffff) {
+              const int base = j + q * window + slice;
+              const bool valid = base + lane < end;
+              DepRec nx;
+              const int nidx = base + window + lane;
+              if (q + 1 < width && nidx < end) nx = rec_at(deprec, dep_pix, nidx);
+              V3 o = c;
+              bool h = false;
+              if (valid) {
+                int zero = 0;
+                o = carry_path(sc, cur, maxrec, c, zero, h);
+              }
+              cur = nx;
+              hmq[q] = __ballot(valid && h);
+              const unsigned long long m = __ballot(valid && !same_bits(o, c));
+              if (m) {
+                const int k = __ffsll((long long)m) - 1;
+                wpos = base + k;
+                wo = v3(__shfl(o.x, k, 64), __shfl(o.y, k, 64), __shfl(o.z, k, 64));
+              }
+            }
           }
-          const unsigned long long m = __ballot(valid && !same_bits(o, c));
-          const int k = m ? __ffsll((long long)m) - 1 : -1;
-          if (lane == 0) s_pos[wave] = k >= 0 ? base + k : 0x7fffffff;
-          if (k >= 0 && lane == k) {
-            s_o[wave][0] = o.x;
-            s_o[wave][1] = o.y;
-            s_o[wave][2] = o.z;
+          if (lane == 0) {
+            s_pos[wave] = wpos;
+            s_o[wave][0] = wo.x;
+            s_o[wave][1] = wo.y;
+            s_o[wave][2] = wo.z;
           }
           __syncthreads();
           if (threadIdx.x == 0) {
@@ -1795,21 +1822,27 @@ __global__ void __launch_bounds__(kResolveBlock) k_resolve(
           }
           __syncthreads();
           const int gpos = s_gpos;
-          // entries before the first changer, and the changer itself, read carry c
-          {
-            // entries up to the first changer (gpos = 0x7fffffff: none in this round)
-            const long long hi0 = end - base < 64 ? end - base : 64;
-            const long long hi1 = (long long)gpos - base + 1;
-            const int hi = (int)(hi1 < hi0 ? hi1 : hi0);
-            const unsigned long long hm = __ballot(valid && h);
-            if (hi > 0) cin_put_wave_uniform(cin, base, 0, hi, c, tag, hm);
+          // entries before the first changer, and the changer itself, read carry c (gpos =
+          // 0x7fffffff: every entry of the round); a wave that stopped early has no entry
+          // at or before gpos in its later sub-windows
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            if (q < width) {
+              const int base = j + q * window + slice;
+              const long long hi0 = end - base < 64 ? end - base : 64;
+              const long long hi1 = (long long)gpos - base + 1;
+              const int hi = (int)(hi1 < hi0 ? hi1 : hi0);
+              if (hi > 0) cin_put_wave_uniform(cin, base, 0, hi, c, tag, hmq[q]);
+            }
           }
           if (gpos == 0x7fffffff) {
-            j += window;
+            j += width * window;
+            width = width < 4 ? 2 * width : 4;
           } else {
             j = gpos + 1;
             c = v3(s_nc[0], s_nc[1], s_nc[2]);
             resolve = true;
+            width = 1;
           }
           __syncthreads();
         } else {
@@ -2629,7 +2662,7 @@ hipError_t launch_parity(const LaunchScene& s, int W, int H, int maxrec, uint8_t
                      w.seg_key);
   hipLaunchKernelGGL(k_seg_order, dim3(1), dim3(1024), 0, stream, w.seg_start, w.counters,
                      w.seg_order, w.batch_state, w.batch_cnt, w.batch_rq, w.block_min,
-                     w.batch_ints > 0 ? 0 : 1);
+                     w.resolve_blocks - w.team_blocks - w.helpers, w.batch_ints > 0 ? 0 : 1);
   // resolve_lds > 80 KiB keeps one resolver block (4 waves, one per SIMD) per CU: the chain
   // steps are latency-bound, so a resolver wave should not share its SIMD
   if (ev) (void)hipEventRecord(ev[1], stream);
@@ -2813,7 +2846,8 @@ hipError_t launch_shard_resolve(const LaunchScene& s, int W, int H, int G, int r
                      w.row_prevw, w.row_prevd, (DepRec*)w.deprec, w.dep_pix, w.seg_start,
                      w.seg_key, w.wcarry, bound);
   hipLaunchKernelGGL(k_seg_order, dim3(1), dim3(1024), 0, stream, w.seg_start, w.counters,
-                     w.seg_order, w.batch_state, w.batch_cnt, w.batch_rq, w.block_min, 1);
+                     w.seg_order, w.batch_state, w.batch_cnt, w.batch_rq, w.block_min,
+                     w.resolve_blocks - w.team_blocks - w.helpers, 1);
   if (ev) (void)hipEventRecord(ev[0], stream);
   auto kres = s.n <= kLdsShapes ? k_resolve<true> : k_resolve<false>;
   hipLaunchKernelGGL(kres, dim3(w.resolve_blocks), dim3(kResolveBlock), w.resolve_lds, stream,
