@@ -61,6 +61,8 @@ SCHEDULES = {"no-side": dict(side=0), "side-always": dict(side=1), "side-by-size
              "in-resolver+no-dep-fast": dict(side=3, dep_fast=0),
              "in-resolver+no-helpers": dict(side=3, helpers=0),
              "in-resolver-until-done": dict(side=4),
+             "no-block-segments": dict(block_min=0),
+             "block-segments-256": dict(block_min=256),
              "split-shade": dict(split_shade=1, side=1),
              "resolve-shared": dict(resolve_shared=1), "no-dep-fast": dict(dep_fast=0),
              "no-side+no-dep-fast": dict(side=0, dep_fast=0),
