@@ -79,22 +79,41 @@ PMC_PROFILES = {("quadric", 4096, 6, "parity"): "profiles/r03b_pmc_lone_4096.jso
                 ("quadric", 4096, 6, "fast"): "profiles/r02c_pmc_fast_4096.json"}
 
 
-def pmc_kernel(kernel, scene, size, depth, mode):
+# FETCH/WRITE of the frames-in-flight launches themselves (scripts/pmc_traffic.py over the
+# bench's timed launches): a pipeline lane's resolver has no phase C inside, so its traffic
+# differs from the lone frame's
+PMC_TRAFFIC_INFLIGHT = {("quadric", 4096, 6, "parity"): "profiles/r03d_pmc_traffic_inflight_4096.json"}
+
+
+def pmc_kernel(kernel, scene, size, depth, mode, inflight=False):
     """Counter means of `kernel` from the committed PMC summary of this configuration:
     hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 per launch (the gfx950 correction of
     MI355X_MICROARCH.md), write_bytes = WRITE_SIZE * 1024, valu_busy; (None, None) when no
-    profile covers it."""
+    profile covers it.  inflight: hbm_bytes from the frames-in-flight traffic summary when one
+    exists (valu_busy stays the lone frame's)."""
+    def find(rel):
+        if not rel or not os.path.exists(os.path.join(ROOT, rel)):
+            return None
+        with open(os.path.join(ROOT, rel)) as f:
+            prof = json.load(f)
+        for name, d in prof["kernels"].items():
+            if name.split("::")[-1].split("<")[0] == kernel:
+                return d
+        return None
     rel = PMC_PROFILES.get((scene, size, depth, mode))
-    if not rel or not os.path.exists(os.path.join(ROOT, rel)):
+    d = find(rel)
+    if d is None:
         return None, None
-    with open(os.path.join(ROOT, rel)) as f:
-        prof = json.load(f)
-    for name, d in prof["kernels"].items():
-        if name.split("::")[-1].split("<")[0] == kernel:
-            return {"hbm_bytes": d.get("hbm_bytes"),
-                    "write_bytes": d["WRITE_SIZE"] * 1024 if "WRITE_SIZE" in d else None,
-                    "valu_busy": d.get("valu_busy")}, rel
-    return None, None
+    out = {"hbm_bytes": d.get("hbm_bytes"),
+           "write_bytes": d["WRITE_SIZE"] * 1024 if "WRITE_SIZE" in d else None,
+           "valu_busy": d.get("valu_busy")}
+    if inflight:
+        trel = PMC_TRAFFIC_INFLIGHT.get((scene, size, depth, mode))
+        t = find(trel)
+        if t is not None:
+            out["hbm_bytes"] = t.get("hbm_bytes")
+            rel = f"{trel} (traffic); {rel} (valu_busy, lone frame)"
+    return out, rel
 
 
 def end_to_end(pkg, scene, W, H, depth, mode, reps=5):
@@ -550,7 +569,8 @@ def main():
         # per step: the dominant kernel's algorithmic work of one image over the step time
         # (with frames in flight two resolvers overlap, so per-launch and per-step differ)
         ach_step = (dom_flop * images / world) / (step_ms * 1e-3) / 1e12 if dom_flop else None
-        pmc, pmc_src = pmc_kernel(dom_name, args.scene, args.size, args.depth, mode)
+        pmc, pmc_src = pmc_kernel(dom_name, args.scene, args.size, args.depth, mode,
+                                  inflight=piped)
         store_name = "k_phase_a" if parity else "k_render"   # the framebuffer's writer
         spmc, spmc_src = pmc_kernel(store_name, args.scene, args.size, args.depth, mode)
         store_ms = phases["phase_a_ms"] if parity else phases["render_ms"]

@@ -1,8 +1,5 @@
 mkdir -p gpurun_out
-SIZE=4096 CHECK=1 TAG="lone4096 default" REPS=10 timeout -k 10 60 python -u scripts/lone.py || exit 1
-SIZE=4096 CHECK=1 TAG="lone4096 bands" TUNE=bands=1 REPS=10 timeout -k 10 60 python -u scripts/lone.py || exit 1
-SIZE=4096 CHECK=1 TAG="lone4096 bands1024" TUNE=bands=1024 REPS=10 timeout -k 10 60 python -u scripts/lone.py || exit 1
-for cfg in "reflection 2048 4" "simple 1024 6" "quadric 2048 6"; do set -- $cfg
-  SCENE=$1 SIZE=$2 DEPTH=$3 CHECK=1 TAG="$cfg bands" TUNE=bands=1 REPS=10 timeout -k 10 60 python -u scripts/lone.py || exit 1
-done
-SIZE=8192 CHECK=1 TAG="lone8192 bands" TUNE=bands=1 REPS=3 timeout -k 10 90 python -u scripts/lone.py || exit 1
+for i in 1 2; do for t in "" "--tune comp_stream=1"; do
+  echo "== $t"; timeout -k 10 200 python -u bench.py --timed-only --no-cpu-baseline --steps 40 --warmup 3 $t > gpurun_out/b.log 2>&1 || { tail -5 gpurun_out/b.log; exit 1; }
+  tail -1 gpurun_out/b.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'], d['roofline']['kernel_ms'], d['verified']['frames'], d['roofline']['traffic'], d['roofline']['pmc_source'])"
+done; done
