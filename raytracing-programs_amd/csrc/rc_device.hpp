@@ -193,6 +193,11 @@ __device__ __forceinline__ double pow20(double x) {
 // pow(a, n) for an integer spot exponent (C/raycast.c:695), a = (double)float.
 __device__ __forceinline__ double pown_dd(double a, int n) {
   if (n == 0) return 1.0;
+  // a = (double)float: a and a*a are exact doubles (24 and 48 significant bits), which the
+  // double-double loop below would return rounded — the same value, ~15 f64 operations less
+  // (the examples' spot lights use angular-a0 2)
+  if (n == 1) return a;
+  if (n == 2) return a * a;
   unsigned e = n < 0 ? (unsigned)(-n) : (unsigned)n;
   DD base{a, 0.0}, acc{1.0, 0.0};
   while (e) {
