@@ -576,7 +576,9 @@ __device__ __forceinline__ V3 shade(const Scene& sc, int idx, V3 P, V3 N, V3 D, 
     const rc_light& L = sc.lights[l];
     V3 ld = v3(L.pos[0] - P.x, L.pos[1] - P.y, L.pos[2] - P.z);
     const float dist = length(ld);
-    ld = normalize(ld, zero_events);
+    // normalize(ld, zero_events) with its length taken from dist (the same operations)
+    if (dist == 0.0f) zero_events++;
+    else ld = div3(ld, dist);
     // radial attenuation C/raycast.c:666-669
     const float lin = L.r0 + L.r1 * dist;
     const float rad =
