@@ -376,116 +376,158 @@ __global__ void __launch_bounds__(256) k_row_stats(const uint8_t* __restrict__ c
     const int n = W - xc < kRowChunk ? W - xc : kRowChunk;
     if (on) stage_row_chunk(cls + base + xc, n, s_row[wave], lane);
     __syncthreads();
-    for (int x0 = xc; on && x0 < xc + n; x0 += 64) {
+    // unrolled so that the next sub-chunks' LDS reads issue before this one's ballots
+#pragma unroll 8
+    for (int x0 = xc; x0 < (on ? xc + n : xc); x0 += 64) {
       const int x = x0 + lane;
       const uint8_t c = x < W ? s_row[wave][x - xc] : kClsIdent;
       const unsigned long long md = __ballot(c == kClsDep), mw = __ballot(c == kClsWriter);
-      // a DEP lane (not the row's first DEP) starts a segment when a writer lies between it
-      // and the previous DEP: last writer before it > previous DEP before it
-      long long kw = (mw & lt) ? base + x0 + hi_bit(mw & lt) : lw;
-      long long pd = (md & lt) ? base + x0 + hi_bit(md & lt) : ld;
-      const bool st = c == kClsDep && pd >= 0 && kw > pd;
-      ns += __popcll(__ballot(st));
-      if (wf < 0 && ld < 0 && md) {   // first DEP of the row is in this chunk
-        const int f = __ffsll((long long)md) - 1;
-        const unsigned long long wb = mw & ((f ? (~0ull >> (64 - f)) : 0ull));
-        wf = wb ? base + x0 + hi_bit(wb) : lw;
+      if (md) {   // (half the image's rows hold no DEP pixel: their chunks skip this part)
+        // a DEP lane (not the row's first DEP) starts a segment when a writer lies between it
+        // and the previous DEP: last writer before it > previous DEP before it
+        const long long kw = (mw & lt) ? base + x0 + hi_bit(mw & lt) : lw;
+        const long long pd = (md & lt) ? base + x0 + hi_bit(md & lt) : ld;
+        const bool st = c == kClsDep && pd >= 0 && kw > pd;
+        ns += __popcll(__ballot(st));
+        if (wf < 0 && ld < 0) {   // first DEP of the row is in this chunk
+          const int f = __ffsll((long long)md) - 1;
+          const unsigned long long wb = mw & ((f ? (~0ull >> (64 - f)) : 0ull));
+          wf = wb ? base + x0 + hi_bit(wb) : lw;
+        }
+        nd += __popcll(md);
+        ld = base + x0 + hi_bit(md);
       }
-      nd += __popcll(md);
       if (mw) lw = base + x0 + hi_bit(mw);
-      if (md) ld = base + x0 + hi_bit(md);
     }
     __syncthreads();   // the chunk buffer is refilled
   }
   if (on && lane == 0) rs[y] = RowStats{nd, ns, lw, ld, wf};
 }
 
-// One workgroup of 1024: chunks of 1024 rows, wave-level inclusive scans + a carry.
+// One workgroup of 1024: chunks of 4096 rows, four consecutive rows per thread (their loads
+// issued together), a thread-level pass, block scans of the thread totals + a chunk carry.
+// (One row per thread took four dependent load/scan/store rounds at 4096 rows: 16 us.)
+constexpr int kScanRows = 4;
+
+// block-wide exclusive scan of (sum, max, max) over the 1024 threads; returns the block
+// totals in t_cnt / t_w / t_d
+__device__ __forceinline__ void block_scan3(int& cnt, long long& lw, long long& ld, int* w_cnt,
+                                            long long* w_w, long long* w_d, int& t_cnt,
+                                            long long& t_w, long long& t_d) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int c = cnt;
+  long long a = lw, d = ld;
+  for (int o = 1; o < 64; o <<= 1) {   // inclusive wave scans
+    const int c2 = __shfl_up(c, o, 64);
+    const long long a2 = __shfl_up(a, o, 64), d2 = __shfl_up(d, o, 64);
+    if (lane >= o) {
+      c += c2;
+      a = a2 > a ? a2 : a;
+      d = d2 > d ? d2 : d;
+    }
+  }
+  if (lane == 63) {
+    w_cnt[wave] = c;
+    w_w[wave] = a;
+    w_d[wave] = d;
+  }
+  __syncthreads();
+  int pc = 0;
+  long long pw = -1, pd = -1;
+  for (int q = 0; q < wave; ++q) {
+    pc += w_cnt[q];
+    pw = w_w[q] > pw ? w_w[q] : pw;
+    pd = w_d[q] > pd ? w_d[q] : pd;
+  }
+  t_cnt = 0;
+  t_w = -1;
+  t_d = -1;
+  for (int q = 0; q < 16; ++q) {
+    t_cnt += w_cnt[q];
+    t_w = w_w[q] > t_w ? w_w[q] : t_w;
+    t_d = w_d[q] > t_d ? w_d[q] : t_d;
+  }
+  // exclusive: the wave prefix combined with the lanes before this one
+  int ec = __shfl_up(c, 1, 64);
+  long long ea = __shfl_up(a, 1, 64), ed = __shfl_up(d, 1, 64);
+  if (lane == 0) {
+    ec = 0;
+    ea = -1;
+    ed = -1;
+  }
+  cnt = pc + ec;
+  lw = ea > pw ? ea : pw;
+  ld = ed > pd ? ed : pd;
+  __syncthreads();   // the wave totals are rewritten by the next scan
+}
+
 __global__ void __launch_bounds__(1024) k_row_scan(int H, const RowStats* __restrict__ rs,
                                                    int* __restrict__ row_off,
                                                    int* __restrict__ row_soff,
                                                    long long* __restrict__ row_prevw,
                                                    long long* __restrict__ row_prevd,
                                                    int* __restrict__ counters) {
-  __shared__ int w_cnt[16], w_seg[16];
+  __shared__ int w_cnt[16];
   __shared__ long long w_w[16], w_d[16];
-  __shared__ int c_cnt, c_seg;
-  __shared__ long long c_w, c_d;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if (threadIdx.x == 0) {
-    c_cnt = 0;
-    c_seg = 0;
-    c_w = -1;
-    c_d = -1;
-  }
-  __syncthreads();
-  for (int y0 = 0; y0 < H; y0 += 1024) {
-    const int y = y0 + threadIdx.x;
-    RowStats r = y < H ? rs[y] : RowStats{0, 0, -1, -1, -1};
-    // inclusive wave scans: count (sum), last writer / DEP (max)
-    int cnt = r.ndep;
-    long long lw = r.lastw, ld = r.lastd;
-    for (int o = 1; o < 64; o <<= 1) {
-      const int c2 = __shfl_up(cnt, o, 64);
-      const long long w2 = __shfl_up(lw, o, 64), d2 = __shfl_up(ld, o, 64);
-      if (lane >= o) {
-        cnt += c2;
-        lw = w2 > lw ? w2 : lw;
-        ld = d2 > ld ? d2 : ld;
+  int c_cnt = 0, c_seg = 0;           // chunk carries (every thread holds the same values)
+  long long c_w = -1, c_d = -1;
+  for (int y0 = 0; y0 < H; y0 += 1024 * kScanRows) {
+    const int yb = y0 + threadIdx.x * kScanRows;
+    RowStats r[kScanRows];
+#pragma unroll
+    for (int k = 0; k < kScanRows; ++k)
+      r[k] = yb + k < H ? rs[yb + k] : RowStats{0, 0, -1, -1, -1};
+    // thread totals over its rows
+    int cnt = 0;
+    long long lw = -1, ld = -1;
+#pragma unroll
+    for (int k = 0; k < kScanRows; ++k) {
+      cnt += r[k].ndep;
+      lw = r[k].lastw > lw ? r[k].lastw : lw;
+      ld = r[k].lastd > ld ? r[k].lastd : ld;
+    }
+    int t_cnt;
+    long long t_w, t_d;
+    block_scan3(cnt, lw, ld, w_cnt, w_w, w_d, t_cnt, t_w, t_d);
+    // this thread's exclusive prefix, with the chunk carry
+    int pc = c_cnt + cnt;
+    long long pw = lw > c_w ? lw : c_w, pdd = ld > c_d ? ld : c_d;
+    // per row: exclusive values, the first DEP's start decision, segment counts
+    int nseg[kScanRows];
+    int segsum = 0;
+#pragma unroll
+    for (int k = 0; k < kScanRows; ++k) {
+      nseg[k] = r[k].nstart;
+      if (r[k].ndep > 0) {
+        const long long key = r[k].wfirst > pw ? r[k].wfirst : pw;
+        if (pdd < 0 || key > pdd) nseg[k] += 1;
       }
+      if (yb + k < H) {
+        row_off[yb + k] = pc;
+        row_prevw[yb + k] = pw;
+        row_prevd[yb + k] = pdd;
+      }
+      pc += r[k].ndep;
+      pw = r[k].lastw > pw ? r[k].lastw : pw;
+      pdd = r[k].lastd > pdd ? r[k].lastd : pdd;
+      segsum += nseg[k];
     }
-    if (lane == 63) {
-      w_cnt[wave] = cnt;
-      w_w[wave] = lw;
-      w_d[wave] = ld;
+    // segment offsets: a second block scan (sum)
+    int sc = segsum;
+    long long dw = -1, dd = -1;
+    int t_seg;
+    long long u1, u2;
+    block_scan3(sc, dw, dd, w_cnt, w_w, w_d, t_seg, u1, u2);
+    int ps = c_seg + sc;
+#pragma unroll
+    for (int k = 0; k < kScanRows; ++k) {
+      if (yb + k < H) row_soff[yb + k] = ps;
+      ps += nseg[k];
     }
-    __syncthreads();
-    int pc = c_cnt;
-    long long pw = c_w, pdd = c_d;
-    for (int q = 0; q < wave; ++q) {
-      pc += w_cnt[q];
-      pw = w_w[q] > pw ? w_w[q] : pw;
-      pdd = w_d[q] > pdd ? w_d[q] : pdd;
-    }
-    // exclusive values for this row
-    const int exc_cnt = pc + cnt - r.ndep;
-    long long exw = __shfl_up(lw, 1, 64), exd = __shfl_up(ld, 1, 64);
-    if (lane == 0) {
-      exw = -1;
-      exd = -1;
-    }
-    exw = exw > pw ? exw : pw;
-    exd = exd > pdd ? exd : pdd;
-    // the row's first DEP: its writer key and the DEP before it decide whether it starts one
-    int nseg = r.nstart;
-    if (r.ndep > 0) {
-      const long long key = r.wfirst > exw ? r.wfirst : exw;
-      if (exd < 0 || key > exd) nseg += 1;
-    }
-    // segment offsets: a second scan (sum)
-    int sc = nseg;
-    for (int o = 1; o < 64; o <<= 1) {
-      const int s2 = __shfl_up(sc, o, 64);
-      if (lane >= o) sc += s2;
-    }
-    if (lane == 63) w_seg[wave] = sc;
-    __syncthreads();
-    int ps = c_seg;
-    for (int q = 0; q < wave; ++q) ps += w_seg[q];
-    if (y < H) {
-      row_off[y] = exc_cnt;
-      row_soff[y] = ps + sc - nseg;
-      row_prevw[y] = exw;
-      row_prevd[y] = exd;
-    }
-    __syncthreads();
-    if (threadIdx.x == 1023) {
-      c_cnt = pc + cnt;
-      c_seg = ps + sc;
-      c_w = lw > pw ? lw : pw;
-      c_d = ld > pdd ? ld : pdd;
-    }
-    __syncthreads();
+    c_cnt += t_cnt;
+    c_seg += t_seg;
+    c_w = t_w > c_w ? t_w : c_w;
+    c_d = t_d > c_d ? t_d : c_d;
   }
   if (threadIdx.x == 0) {
     counters[0] = c_seg;
@@ -511,7 +553,8 @@ __global__ void __launch_bounds__(256) k_row_compact(
     const int n = W - xc < kRowChunk ? W - xc : kRowChunk;
     if (on) stage_row_chunk(cls + base + xc, n, s_row[wave], lane);
     __syncthreads();
-    for (int x0 = xc; on && x0 < xc + n; x0 += 64) {
+#pragma unroll 8
+    for (int x0 = xc; x0 < (on ? xc + n : xc); x0 += 64) {
       const int x = x0 + lane;
       const uint8_t c = x < W ? s_row[wave][x - xc] : kClsIdent;
       const unsigned long long md = __ballot(c == kClsDep), mw = __ballot(c == kClsWriter);
