@@ -73,16 +73,16 @@ def load_pkg():
 
 # rocprofv3 --pmc summaries of this exact configuration from HEAD (scripts/pmc_valu.sh,
 # scripts/pmc_fast.sh -> scripts/pmc_summary.py): per-kernel counter means per launch.
-PMC_PROFILES = {("quadric", 4096, 6, "parity"): "profiles/r03b_pmc_lone_4096.json",
-                ("reflection", 2048, 4, "parity"): "profiles/r03b_pmc_lone_c3.json",
-                ("quadric", 8192, 6, "parity"): "profiles/r03b_pmc_lone_c5.json",
+PMC_PROFILES = {("quadric", 4096, 6, "parity"): "profiles/r03e_pmc_lone_4096.json",
+                ("reflection", 2048, 4, "parity"): "profiles/r03e_pmc_lone_c3.json",
+                ("quadric", 8192, 6, "parity"): "profiles/r03e_pmc_lone_c5.json",
                 ("quadric", 4096, 6, "fast"): "profiles/r02c_pmc_fast_4096.json"}
 
 
 # FETCH/WRITE of the frames-in-flight launches themselves (scripts/pmc_traffic.py over the
 # bench's timed launches): a pipeline lane's resolver has no phase C inside, so its traffic
 # differs from the lone frame's
-PMC_TRAFFIC_INFLIGHT = {("quadric", 4096, 6, "parity"): "profiles/r03d_pmc_traffic_inflight_4096.json"}
+PMC_TRAFFIC_INFLIGHT = {("quadric", 4096, 6, "parity"): "profiles/r03e_pmc_traffic_inflight_4096.json"}
 
 
 def pmc_kernel(kernel, scene, size, depth, mode, inflight=False):
