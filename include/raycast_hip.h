@@ -280,6 +280,8 @@ typedef struct rc_tuning {
                              waves shade ready batches) instead of on the pixel partition:
                              0 never (default), 1 until the queue is drained, 2 until the
                              lane's own resolver work is over (k_finish shades the rest)     */
+  int x0;                 /* 1: quadrics whose d, e, f are all zero are tested without their
+                             cross terms (bit-identical, rc_device.hpp quad_abc; default 1) */
 } rc_tuning;
 void rc_default_tuning(rc_tuning *t);
 int rc_set_tuning(const rc_tuning *t);

@@ -97,8 +97,24 @@ static int o_sphere(const float *O, const float *D, const shape_t *s, float *t) 
   return 1;
 }
 
+/* Diagnostic for the tests (not part of the reference's algorithm): tests of a quadric without
+ * cross terms (d = e = f = 0) in which a cross term is NaN — the case the HIP kernels handle by
+ * rejecting the quadric (rc_device.hpp x0_reject).  Not thread-safe; read by the tests only. */
+static long long g_cross_nan;
+long long rco_cross_nan_events(int reset) {
+  long long v = g_cross_nan;
+  if (reset) g_cross_nan = 0;
+  return v;
+}
+
 /* C/raycast.c:614-656 — the double accumulations follow the source's left-to-right order */
 static int o_quadric(const float *O, const float *D, const shape_t *q, float *t) {
+  if (q->d == 0.0f && q->e == 0.0f && q->f == 0.0f &&
+      (isnan(q->d * D[0] * D[1]) || isnan(q->e * D[0] * D[2]) || isnan(q->f * D[1] * D[2]) ||
+       isnan(q->d * (O[0] * D[1] + O[1] * D[0])) || isnan(q->e * (O[0] * D[2] + O[2] * D[0])) ||
+       isnan(q->f * (O[1] * D[2] + O[2] * D[1])) || isnan(q->d * O[0] * O[1]) ||
+       isnan(q->e * O[0] * O[2]) || isnan(q->f * O[1] * O[2])))
+    g_cross_nan++;
   const double A = q->a, B = q->b, C = q->c;
   double acc;
   /* a_q (C/raycast.c:615-617) */

@@ -64,6 +64,7 @@ rc_tuning default_tuning() {
   t.side_blocks = 0;
   t.comp_stream = 2;
   t.pipe_inres = 0;
+  t.x0 = 1;
   // regular segments of >= 3000 entries on whole workgroups when there are workgroups for all
   // of them (k_seg_order): lone quadric 4096^2 5.19 -> 5.06 ms (its ~100 3856-entry segments
   // 4.4 -> 2.5 ms, under the team segment); 8192^2 and pipeline lanes have more such segments
@@ -475,8 +476,13 @@ int upload_scene(FrameBufs& b, hipStream_t stream, const rc_scene* s, rc::Launch
   const rc_shape* hs = (const rc_shape*)((const char*)h + h->off_shapes);
   for (int k = 0; k < h->n && k < 64; ++k)
     if (hs[k].refl > 0.0f) ls.refl_mask |= 1ull << k;
+  bool cross = false;   // some quadric has cross terms (d, e, f)
   for (int k = 0; k < h->n; ++k)
-    if (hs[k].type == RC_SHAPE_QUADRIC) ls.has_quadric = 1;
+    if (hs[k].type == RC_SHAPE_QUADRIC) {
+      ls.has_quadric = 1;
+      if (hs[k].qd != 0.0f || hs[k].qe != 0.0f || hs[k].qf != 0.0f) cross = true;
+    }
+  if (ls.has_quadric && !cross && tune().x0) ls.has_quadric = 2;   // rc_device.hpp quad_x0
   // Clean DEP entries' colour = phase A's primary shade exactly when every bounce level's
   // shade of them is zero: the phantom (shapes_list[-1], index n) is black, and the
   // reflectivity product T stays finite (0 * T == 0).

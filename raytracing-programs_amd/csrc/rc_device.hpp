@@ -43,7 +43,8 @@ struct Scene {
   const rc_shade_pair* lpairs;
   int n, m;
   unsigned long long refl_mask;          // bit k: shape k has reflectivity > 0 (k < 64)
-  int has_quadric;                       // any quadric: picks the evaluator specialisation
+  int has_quadric;                       // any quadric: picks the evaluator specialisation;
+                                         // 2: none of them has cross terms (quad_x0)
   int o0_ok;                             // primary rays may use rc_shape::o0 (nearest_primary)
   // Clean DEP entries (no bounce level hits at their carry-in) take their colour from phase
   // A's primary shade: set when every level's shade of such an entry is exactly zero (black
@@ -252,40 +253,80 @@ __device__ __forceinline__ bool hit_plane(V3 O, V3 D, const rc_shape& s, float& 
   return true;
 }
 
-// C/raycast.c:614-656 — double accumulations in source order, float products as written
-__device__ __forceinline__ bool hit_quadric(V3 O, V3 D, const rc_shape& q, float& t) {
+// Quadrics without cross terms (d = e = f = 0 for every quadric of the scene, as in every
+// example scene; quad_x0).  Each cross term is (+-0 coefficient) * (float operands):
+//   a: (qd*D.x)*D.y, (qe*D.x)*D.z, (qf*D.y)*D.z      NaN iff some D component is inf/NaN
+//   c: (qd*O.x)*O.y, (qe*O.x)*O.z, (qf*O.y)*O.z      NaN iff some O component is inf/NaN
+//   b: qd*(O.x*D.y + O.y*D.x), qe*(..), qf*(..)      NaN iff one of the three float sums is
+//                                                    inf/NaN
+// and +-0 otherwise.  Adding +-0 to a double accumulator leaves it unchanged unless it is
+// itself zero, so dropping the terms can change only the SIGN of a zero a, b or c, which no
+// result of the test sees: a zero a takes the linear branch either way, b enters the
+// discriminant squared and the roots as -b +- sqrt(disc) (a zero sqrt makes both roots +-0,
+// rejected by t > 0), a zero b in the linear branch gives t = +-inf or NaN (rejected by
+// best > t / t > 0), and a zero c makes 4ac = +-0, which leaves b*b unchanged.  A NaN term
+// makes a, b or c NaN, and then every branch of the test ends in t = NaN, which every caller
+// rejects (best > t, t > 0, quot_class).  So the short form plus one per-ray flag —
+// x0_reject: some cross term would be NaN, the quadric is rejected — is bit-identical.
+__device__ __forceinline__ bool quad_x0(const Scene& sc) { return sc.has_quadric == 2; }
+__device__ __forceinline__ bool nonfinite3(float a, float b, float c) {
+  return !__builtin_isfinite(a) | !__builtin_isfinite(b) | !__builtin_isfinite(c);
+}
+__device__ __forceinline__ bool x0_reject(V3 O, V3 D) {
+  return nonfinite3(D.x, D.y, D.z) | nonfinite3(O.x, O.y, O.z) |
+         nonfinite3(O.x * D.y + O.y * D.x, O.x * D.z + O.z * D.x, O.y * D.z + O.z * D.y);
+}
+
+// The quadric's a, b, c (C/raycast.c:614-641): double accumulations in source order, float
+// products as written; kX0 drops the cross terms (quad_x0 with x0_reject, above).
+__device__ __forceinline__ void quad_abc(V3 O, V3 D, const rc_shape& q, float& aq, float& bq,
+                                         float& cq, bool x0) {
+  // c, a, b: the order the resolver's evaluator has always used (its schedule is sensitive)
   double acc;
-  acc = q.A * ((double)D.x * (double)D.x);
-  acc = acc + q.B * ((double)D.y * (double)D.y);
-  acc = acc + q.C * ((double)D.z * (double)D.z);
-  acc = acc + (double)(q.qd * D.x * D.y);
-  acc = acc + (double)(q.qe * D.x * D.z);
-  acc = acc + (double)(q.qf * D.y * D.z);
-  const float aq = (float)acc;
-
-  acc = 2.0 * q.A * (double)O.x * (double)D.x;
-  acc = acc + 2.0 * q.B * (double)O.y * (double)D.y;
-  acc = acc + 2.0 * q.C * (double)O.z * (double)D.z;
-  acc = acc + (double)(q.qd * (O.x * D.y + O.y * D.x));
-  acc = acc + (double)(q.qe * (O.x * D.z + O.z * D.x));
-  acc = acc + (double)(q.qf * (O.y * D.z + O.z * D.y));
-  acc = acc + (double)(q.qg * D.x);
-  acc = acc + (double)(q.qh * D.y);
-  acc = acc + (double)(q.qi * D.z);
-  const float bq = (float)acc;
-
   acc = q.A * ((double)O.x * (double)O.x);
   acc = acc + q.B * ((double)O.y * (double)O.y);
   acc = acc + q.C * ((double)O.z * (double)O.z);
-  acc = acc + (double)(q.qd * O.x * O.y);
-  acc = acc + (double)(q.qe * O.x * O.z);
-  acc = acc + (double)(q.qf * O.y * O.z);
+  if (!x0) {
+    acc = acc + (double)(q.qd * O.x * O.y);
+    acc = acc + (double)(q.qe * O.x * O.z);
+    acc = acc + (double)(q.qf * O.y * O.z);
+  }
   acc = acc + (double)(q.qg * O.x);
   acc = acc + (double)(q.qh * O.y);
   acc = acc + (double)(q.qi * O.z);
   acc = acc + (double)q.qj;
-  const float cq = (float)acc;
+  cq = (float)acc;
 
+  acc = q.A * ((double)D.x * (double)D.x);
+  acc = acc + q.B * ((double)D.y * (double)D.y);
+  acc = acc + q.C * ((double)D.z * (double)D.z);
+  if (!x0) {
+    acc = acc + (double)(q.qd * D.x * D.y);
+    acc = acc + (double)(q.qe * D.x * D.z);
+    acc = acc + (double)(q.qf * D.y * D.z);
+  }
+  aq = (float)acc;
+
+  acc = 2.0 * q.A * (double)O.x * (double)D.x;
+  acc = acc + 2.0 * q.B * (double)O.y * (double)D.y;
+  acc = acc + 2.0 * q.C * (double)O.z * (double)D.z;
+  if (!x0) {
+    acc = acc + (double)(q.qd * (O.x * D.y + O.y * D.x));
+    acc = acc + (double)(q.qe * (O.x * D.z + O.z * D.x));
+    acc = acc + (double)(q.qf * (O.y * D.z + O.z * D.y));
+  }
+  acc = acc + (double)(q.qg * D.x);
+  acc = acc + (double)(q.qh * D.y);
+  acc = acc + (double)(q.qi * D.z);
+  bq = (float)acc;
+}
+
+// C/raycast.c:614-656; x0 = quad_x0 (uniform), rej = x0 && x0_reject(O, D)
+__device__ __forceinline__ bool hit_quadric(V3 O, V3 D, const rc_shape& q, float& t, bool x0,
+                                            bool rej) {
+  float aq, bq, cq;
+  quad_abc(O, D, q, aq, bq, cq, x0);
+  if (rej) return false;
   if ((double)aq == 0.0) {
     t = (float)((-1.0 * (double)cq) / (double)bq);
     return true;
@@ -304,12 +345,12 @@ __device__ __forceinline__ bool hit_quadric(V3 O, V3 D, const rc_shape& q, float
 // shadow-from-phantom rays).  Returns whether the shape would be accepted as a candidate
 // with distance t (before the nearest/positive check).  Type is wave-uniform.
 __device__ __forceinline__ bool test_shape(const rc_shape& s, V3 O, V3 D, RayK rk, int skip,
-                                           float& t) {
+                                           float& t, bool x0 = false, bool rej = false) {
   const int type = s.type;
   if (type == RC_SHAPE_SPHERE) return hit_sphere(O, D, s, rk, t);
   if (type == RC_SHAPE_PLANE) return hit_plane(O, D, s, t);
   if (type == RC_SHAPE_QUADRIC) {
-    if (!hit_quadric(O, D, s, t)) return false;
+    if (!hit_quadric(O, D, s, t, x0, rej)) return false;
     // C/raycast.c:492-494: for bounce rays a quadric hit below the origin's z is ignored
     if (skip != -1 && (O.z + t * D.z) < O.z) return false;
     return true;
@@ -320,11 +361,12 @@ __device__ __forceinline__ bool test_shape(const rc_shape& s, V3 O, V3 D, RayK r
 // C/raycast.c:441-531 (shadow_test = false): index of the nearest accepted shape, its t.
 __device__ __forceinline__ int nearest(const Scene& sc, V3 O, V3 D, int skip, float& tbest) {
   const RayK rk = ray_consts(D);
+  const bool x0 = quad_x0(sc), rej = x0 && x0_reject(O, D);
   float best = __builtin_inff();
   int idx = -1;
   for (int k = 0; k < sc.n; ++k) {
     float t = 0.0f;
-    const bool hit = test_shape(sc.shapes[k], O, D, rk, skip, t);
+    const bool hit = test_shape(sc.shapes[k], O, D, rk, skip, t, x0, rej);
     if (hit && k != skip && best > t && t > 0.0f) {
       best = t;
       idx = k;
@@ -333,7 +375,6 @@ __device__ __forceinline__ int nearest(const Scene& sc, V3 O, V3 D, int skip, fl
   tbest = best;
   return idx;
 }
-
 // ------------------------------------------------------------------ primary rays --
 // The primary ray of every pixel starts at O = (0,0,0) (C/raycast.c:118-121).  Each test's
 // origin-only term is then a per-shape constant (rc_shape::o0, computed on the host by the
@@ -364,14 +405,16 @@ __device__ __forceinline__ bool hit_plane_o0(V3 D, const rc_shape& s, float& t) 
   return true;
 }
 
-__device__ __forceinline__ bool hit_quadric_o0(V3 D, const rc_shape& q, float& t) {
+__device__ __forceinline__ bool hit_quadric_o0(V3 D, const rc_shape& q, float& t, bool x0) {
   double acc;
   acc = q.A * ((double)D.x * (double)D.x);
   acc = acc + q.B * ((double)D.y * (double)D.y);
   acc = acc + q.C * ((double)D.z * (double)D.z);
-  acc = acc + (double)(q.qd * D.x * D.y);
-  acc = acc + (double)(q.qe * D.x * D.z);
-  acc = acc + (double)(q.qf * D.y * D.z);
+  if (!x0) {   // cross terms (quad_x0)
+    acc = acc + (double)(q.qd * D.x * D.y);
+    acc = acc + (double)(q.qe * D.x * D.z);
+    acc = acc + (double)(q.qf * D.y * D.z);
+  }
   const float aq = (float)acc;
   acc = (double)(q.qg * D.x);
   acc = acc + (double)(q.qh * D.y);
@@ -396,6 +439,7 @@ __device__ __forceinline__ bool hit_quadric_o0(V3 D, const rc_shape& q, float& t
 __device__ __forceinline__ int nearest_primary(const Scene& sc, V3 D, float& tbest) {
   if (!sc.o0_ok) return nearest(sc, v3(0.0f, 0.0f, 0.0f), D, -1, tbest);
   const RayK rk = ray_consts(D);
+  const bool x0 = quad_x0(sc), rej = x0 && x0_reject(v3(0.0f, 0.0f, 0.0f), D);
   float best = __builtin_inff();
   int idx = -1;
   for (int k = 0; k < sc.n; ++k) {
@@ -404,7 +448,8 @@ __device__ __forceinline__ int nearest_primary(const Scene& sc, V3 D, float& tbe
     bool hit = false;
     if (s.type == RC_SHAPE_SPHERE) hit = hit_sphere_o0(D, s, rk, t);
     else if (s.type == RC_SHAPE_PLANE) hit = hit_plane_o0(D, s, t);
-    else if (s.type == RC_SHAPE_QUADRIC) hit = hit_quadric_o0(D, s, t);
+    else if (s.type == RC_SHAPE_QUADRIC)
+      hit = hit_quadric_o0(D, s, t, x0) && !rej;
     if (hit && best > t && t > 0.0f) {
       best = t;
       idx = k;
@@ -453,38 +498,11 @@ __device__ __forceinline__ bool shadow_sphere(V3 O, V3 D, const rc_shape& s, Ray
 // hit_quadric + the bounce rays' z rule as a shadow test.  The z rule (C/raycast.c:492-494)
 // needs t itself when it can fire, i.e. for a positive t only if D.z < 0: then the chosen
 // root's quotient is formed exactly as in hit_quadric.
-__device__ __forceinline__ bool shadow_quadric(V3 O, V3 D, const rc_shape& q, int skip) {
-  double acc;
-  acc = q.A * ((double)D.x * (double)D.x);
-  acc = acc + q.B * ((double)D.y * (double)D.y);
-  acc = acc + q.C * ((double)D.z * (double)D.z);
-  acc = acc + (double)(q.qd * D.x * D.y);
-  acc = acc + (double)(q.qe * D.x * D.z);
-  acc = acc + (double)(q.qf * D.y * D.z);
-  const float aq = (float)acc;
-
-  acc = 2.0 * q.A * (double)O.x * (double)D.x;
-  acc = acc + 2.0 * q.B * (double)O.y * (double)D.y;
-  acc = acc + 2.0 * q.C * (double)O.z * (double)D.z;
-  acc = acc + (double)(q.qd * (O.x * D.y + O.y * D.x));
-  acc = acc + (double)(q.qe * (O.x * D.z + O.z * D.x));
-  acc = acc + (double)(q.qf * (O.y * D.z + O.z * D.y));
-  acc = acc + (double)(q.qg * D.x);
-  acc = acc + (double)(q.qh * D.y);
-  acc = acc + (double)(q.qi * D.z);
-  const float bq = (float)acc;
-
-  acc = q.A * ((double)O.x * (double)O.x);
-  acc = acc + q.B * ((double)O.y * (double)O.y);
-  acc = acc + q.C * ((double)O.z * (double)O.z);
-  acc = acc + (double)(q.qd * O.x * O.y);
-  acc = acc + (double)(q.qe * O.x * O.z);
-  acc = acc + (double)(q.qf * O.y * O.z);
-  acc = acc + (double)(q.qg * O.x);
-  acc = acc + (double)(q.qh * O.y);
-  acc = acc + (double)(q.qi * O.z);
-  acc = acc + (double)q.qj;
-  const float cq = (float)acc;
+__device__ __forceinline__ bool shadow_quadric(V3 O, V3 D, const rc_shape& q, int skip, bool x0,
+                                               bool rej) {
+  float aq, bq, cq;
+  quad_abc(O, D, q, aq, bq, cq, x0);
+  if (rej) return false;
 
   double num, den;
   int cls;
@@ -516,6 +534,7 @@ __device__ __forceinline__ bool shadow_quadric(V3 O, V3 D, const rc_shape& q, in
 // such shape is always accepted, so the loop may stop there.
 __device__ __forceinline__ bool shadowed(const Scene& sc, V3 O, V3 D, int skip) {
   const RayK rk = ray_consts(D);
+  const bool x0 = quad_x0(sc), rej = x0 && x0_reject(O, D);
   for (int k = 0; k < sc.n; ++k) {
     if (k == skip) continue;
     const rc_shape& s = sc.shapes[k];
@@ -527,13 +546,12 @@ __device__ __forceinline__ bool shadowed(const Scene& sc, V3 O, V3 D, int skip) 
       float t = 0.0f;
       hit = hit_plane(O, D, s, t) && __builtin_inff() > t && t > 0.0f;
     } else if (type == RC_SHAPE_QUADRIC) {
-      hit = shadow_quadric(O, D, s, skip);
+      hit = shadow_quadric(O, D, s, skip, x0, rej);
     }
     if (hit) return true;
   }
   return false;
 }
-
 // Hit point and normal of the accepted shape (C/raycast.c:461-523).
 __device__ __forceinline__ void hit_frame(const Scene& sc, int idx, V3 O, V3 D, float t, V3& P,
                                           V3& N, int& zero_events) {
@@ -970,7 +988,7 @@ __device__ __forceinline__ unsigned long long stamp_now() {
 
 // test_shape() for any type, branch-free.  kQuad = false: the scene has no quadric, so the
 // quadric part is compiled out (every quadric term below is dead).
-template <bool kQuad>
+template <bool kQuad, bool kX0 = false>
 __device__ __forceinline__ bool test_unified(const rc_shape& s, V3 O, V3 D, RayK rk, int skip,
                                              float& t) {
   const int type = s.type;
@@ -987,7 +1005,11 @@ __device__ __forceinline__ bool test_unified(const rc_shape& s, V3 O, V3 D, RayK
   const float denP = dot(D, v3(s.n[0], s.n[1], s.n[2]));
   float cq = 0.0f, aq = 0.0f, bq = 0.0f, discQ = 0.0f;
   bool lin = false;
-  if constexpr (kQuad) {
+  if constexpr (kQuad && kX0) {
+    quad_abc(O, D, s, aq, bq, cq, true);   // no cross terms (quad_x0)
+  } else if constexpr (kQuad) {
+    // written out in this order (c, a, b): the lone resolver wave's schedule is sensitive to
+    // it (the same terms through quad_abc's a, b, c order: lone resolver 4.22 -> 4.44 ms)
     double acc;
     acc = s.A * ((double)O.x * (double)O.x);
     acc = acc + s.B * ((double)O.y * (double)O.y);
@@ -1017,6 +1039,8 @@ __device__ __forceinline__ bool test_unified(const rc_shape& s, V3 O, V3 D, RayK
     acc = acc + (double)(s.qh * D.y);
     acc = acc + (double)(s.qi * D.z);
     bq = (float)acc;
+  }
+  if constexpr (kQuad) {
     discQ = (float)__builtin_fma((double)bq, (double)bq, -(4.0 * (double)aq * (double)cq));
     lin = (double)aq == 0.0;
   }
@@ -1086,9 +1110,9 @@ __device__ __forceinline__ void hit_frame_sel(const rc_shape& s, V3 O, V3 D, flo
 // levels retire in one step.  The carry creep of dense segments alternates hit/miss, so
 // five levels retire in three steps.  Each step is one basic block (selects, no branches)
 // so the scheduler can overlap the independent chains of a lone wave.  GT = the group size
-// as a compile-time constant (4, 8, 16), or 0 for the runtime value Grt; kQuad = the scene has
-// quadrics (test_unified).
-template <int GT, bool kQuad>
+// as a compile-time constant (4, 8, 16), or 0 for the runtime value Grt; kQ = 0: the scene has
+// no quadric, 1: it has, 2: none of its quadrics has cross terms (quad_x0, quad_abc).
+template <int GT, int kQ>
 __device__ __forceinline__ V3 carry_path_spec(const Scene& sc, const LaneShape& ls, int kself,
                                               int Grt, int half, const DepRec& r, int maxrec,
                                               V3 c, int& zero_events, bool& anyhit
@@ -1097,6 +1121,7 @@ __device__ __forceinline__ V3 carry_path_spec(const Scene& sc, const LaneShape& 
 #endif
 ) {
   (void)zero_events;
+  constexpr bool kQuad = kQ != 0;
   anyhit = false;
   const int G = GT ? GT : Grt;
   constexpr int kNone = 0x7fffffff;
@@ -1118,8 +1143,11 @@ __device__ __forceinline__ V3 carry_path_spec(const Scene& sc, const LaneShape& 
     const int myS = half ? -1 : S;
     const RayK rk = ray_consts(myD);
     float tt = 0.0f;
-    const bool ok = test_unified<kQuad>(ls.s, C, myD, rk, myS, tt) && ls.has && kself != myS &&
-                    __builtin_inff() > tt && tt > 0.0f;
+    // kQ = 2: quadrics without cross terms, rejected where a cross term would be NaN
+    // (quad_abc, x0_reject)
+    const bool tok = test_unified<kQuad, kQ == 2>(ls.s, C, myD, rk, myS, tt) &&
+                     !(kQ == 2 && ls.s.type == RC_SHAPE_QUADRIC && x0_reject(C, myD));
+    const bool ok = tok && ls.has && kself != myS && __builtin_inff() > tt && tt > 0.0f;
     float t = ok ? tt : __builtin_inff();
     int k = ok ? kself : kNone;
     RC_STAMP(1);

@@ -17,7 +17,7 @@ struct LaunchScene {
   int n, m;
   float cam_w, cam_h;
   unsigned long long refl_mask;   // bit k: shape k reflective (n <= 64)
-  int has_quadric;                // the scene has a quadric
+  int has_quadric;                // the scene has a quadric (2: none with cross terms, quad_x0)
   int o0_ok;                      // primary rays may use rc_shape::o0
   int dep_fast;                   // clean DEP entries take phase A's primary shade (Scene)
 };

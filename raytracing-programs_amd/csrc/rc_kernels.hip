@@ -28,6 +28,18 @@
 #include "rc_device.hpp"
 #include "rc_kernels.h"
 
+// Which kernels use the cross-term-free quadric form (quad_x0: Scene::has_quadric == 2,
+// rc_device.hpp quad_abc) when the scene allows it.  A kernel with 0 folds has_quadric to 0/1,
+// so quad_x0 is a constant false there and the form and its branches are compiled out.
+#ifndef RC_X0_PIXEL
+#define RC_X0_PIXEL 1     // k_render, k_phase_a, k_classify
+#endif
+#ifndef RC_X0_PHASE_C
+#define RC_X0_PHASE_C 0   // k_dep_chunks, k_finish, k_side
+#endif
+#ifndef RC_X0_RESOLVE
+#define RC_X0_RESOLVE 0   // k_resolve (its inlined phase C included)
+#endif
 #ifndef RC_PHASE_A_WAVES
 #define RC_PHASE_A_WAVES 4   // waves per SIMD the render kernels are compiled for
 #endif
@@ -185,6 +197,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_
                                                    int row_step, int nrows, int maxrec,
                                                    uint8_t* __restrict__ out,
                                                    unsigned long long* __restrict__ zcount) {
+  if (!RC_X0_PIXEL) sc.has_quadric = sc.has_quadric != 0;   // no cross-term-free form here (RC_X0_*)
   __shared__ StageBuf<kStage> stage;
   __shared__ TileBytes tb;
   tile_init(tb);
@@ -237,6 +250,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_
                                                     float4* __restrict__ wcarry,
                                                     DepRec* __restrict__ deprec,
                                                     unsigned long long* __restrict__ zcount) {
+  if (!RC_X0_PIXEL) sc.has_quadric = sc.has_quadric != 0;   // no cross-term-free form here (RC_X0_*)
   __shared__ StageBuf<kStage> stage;
   __shared__ TileBytes tb;
   tile_init(tb);
@@ -288,6 +302,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_
                                                      uint8_t* __restrict__ cls,
                                                      float4* __restrict__ wcarry,
                                                      DepRec* __restrict__ deprec) {
+  if (!RC_X0_PIXEL) sc.has_quadric = sc.has_quadric != 0;   // no cross-term-free form here (RC_X0_*)
   __shared__ StageBuf<kStage> stage;
   stage_scene<kStage>(sc, stage);
   int lx, ly;
@@ -790,7 +805,8 @@ __device__ __forceinline__ int wave_window(const Scene& sc, int maxrec,
 #else
 #define RC_SPEC1(GT, Q) carry_path_spec<GT, Q>(sc, ls, kself, G, half, ri, maxrec, ce, zero, hg)
 #endif
-#define RC_SPEC(GT) (sc.has_quadric ? RC_SPEC1(GT, true) : RC_SPEC1(GT, false))
+#define RC_SPEC(GT) \
+  (sc.has_quadric ? (quad_x0(sc) ? RC_SPEC1(GT, 2) : RC_SPEC1(GT, 1)) : RC_SPEC1(GT, 0))
     if (act) {
       if (G == 8) oc = RC_SPEC(8);
       else if (G == 4) oc = RC_SPEC(4);
@@ -1118,7 +1134,8 @@ __device__ __forceinline__ void block_window(const Scene& sc, int maxrec, BlockW
 #else
 #define RC_SPEC1(GT, Q) carry_path_spec<GT, Q>(sc, ls, kself, G, half, ri, maxrec, ce, zero, hg)
 #endif
-#define RC_SPEC(GT) (sc.has_quadric ? RC_SPEC1(GT, true) : RC_SPEC1(GT, false))
+#define RC_SPEC(GT) \
+  (sc.has_quadric ? (quad_x0(sc) ? RC_SPEC1(GT, 2) : RC_SPEC1(GT, 1)) : RC_SPEC1(GT, 0))
       if (G == 8) oc = RC_SPEC(8);
       else if (G == 4) oc = RC_SPEC(4);
       else if (G == 16) oc = RC_SPEC(16);
@@ -1215,7 +1232,8 @@ __device__ __forceinline__ void block_window(const Scene& sc, int maxrec, BlockW
 #else
 #define RC_SPEC1(GT, Q) carry_path_spec<GT, Q>(sc, ls, kself, G, half, ri, maxrec, c, zero, hg)
 #endif
-#define RC_SPEC(GT) (sc.has_quadric ? RC_SPEC1(GT, true) : RC_SPEC1(GT, false))
+#define RC_SPEC(GT) \
+  (sc.has_quadric ? (quad_x0(sc) ? RC_SPEC1(GT, 2) : RC_SPEC1(GT, 1)) : RC_SPEC1(GT, 0))
       if (act) {
         if (G == 8) oc = RC_SPEC(8);
         else if (G == 4) oc = RC_SPEC(4);
@@ -1699,6 +1717,7 @@ __global__ void __launch_bounds__(kResolveBlock) __attribute__((amdgpu_waves_per
     int helpers, int hand_run, int inject, int block_min, int* __restrict__ rq_cnt,
     int* __restrict__ rq, Cam cam, int W, uint8_t* __restrict__ out, uint32_t* __restrict__ patch,
     unsigned long long* __restrict__ zcount, int* __restrict__ batch_state, int inres) {
+  if (!RC_X0_RESOLVE) sc.has_quadric = sc.has_quadric != 0;   // no cross-term-free form here (RC_X0_*)
   // census for phase C's side kernel: it only proceeds once every resolver block is resident
   if (threadIdx.x == 0)
     __hip_atomic_fetch_add(&counters[5], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2264,6 +2283,7 @@ __global__ void __launch_bounds__(kSideBlock) k_side(
     uint32_t* __restrict__ patch, unsigned long long* __restrict__ zcount,
     TeamState* __restrict__ ts, int resolve_blocks, unsigned tag, int tiles,
     unsigned* __restrict__ trace) {
+  if (!RC_X0_PHASE_C) sc.has_quadric = sc.has_quadric != 0;   // no cross-term-free form here (RC_X0_*)
   __shared__ int s_go;
   __shared__ StageBuf<kStage> stage;
   stage_scene<kStage>(sc, stage);
@@ -2315,6 +2335,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_
     int* __restrict__ batch_state, uint8_t* __restrict__ out, uint32_t* __restrict__ patch,
     unsigned long long* __restrict__ zcount, TeamState* __restrict__ ts, unsigned tag,
     int tiles, const int* __restrict__ rq) {
+  if (!RC_X0_PHASE_C) sc.has_quadric = sc.has_quadric != 0;   // no cross-term-free form here (RC_X0_*)
   // every batch already shaded through the ready queue (the usual case when the resolver's
   // own waves shade them): nothing to stage or claim
   if (rq && !tiles &&
@@ -2365,6 +2386,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_
     const int* __restrict__ counters, uint8_t* __restrict__ out, uint32_t* __restrict__ patch,
     unsigned long long* __restrict__ zcount, TeamState* __restrict__ ts, unsigned tag,
     int limit) {
+  if (!RC_X0_PHASE_C) sc.has_quadric = sc.has_quadric != 0;   // no cross-term-free form here (RC_X0_*)
   __shared__ StageBuf<kStage> stage;
   __shared__ int s_j[kChunk];
   __shared__ float s_c[kChunk][3];

@@ -50,6 +50,8 @@ def oracle_lib():
                                    ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
                                    ctypes.POINTER(RcoStats), ctypes.c_void_p]
         lib.rco_load_scene.argtypes = [ctypes.c_char_p, ctypes.POINTER(rc.JsonDataT)]
+        lib.rco_cross_nan_events.argtypes = [ctypes.c_int]
+        lib.rco_cross_nan_events.restype = ctypes.c_longlong
         lib.rco_free_scene.argtypes = [ctypes.POINTER(rc.JsonDataT)]
         lib.rco_render_cuda.argtypes = [ctypes.POINTER(rc.JsonDataT), ctypes.c_int, ctypes.c_int,
                                         ctypes.c_int, ctypes.c_void_p]
@@ -155,9 +157,10 @@ def scene_path(name):
     return os.path.join(SCENES, name + ".scene")
 
 
-def random_scene(rng, path, n_shapes, n_lights):
+def random_scene(rng, path, n_shapes, n_lights, cross=False):
     """A phantom-safe random scene in the reference grammar (lights keep the phantom black:
-    1 light with color[0]+color[1] >= 1; 2 lights with L1.pos.y + L1.pos.z >= 1)."""
+    1 light with color[0]+color[1] >= 1; 2 lights with L1.pos.y + L1.pos.z >= 1).  cross:
+    quadrics get non-zero cross coefficients d, e, f (the examples' are all zero)."""
     lines = ["camera, width: 2.0, height: 2.0"]
     for _ in range(n_shapes):
         kind = rng.choice(["sphere", "sphere", "plane", "quadric"])
@@ -179,8 +182,10 @@ def random_scene(rng, path, n_shapes, n_lights):
         else:
             a, b, c = rng.uniform(-1, 4, 3)
             g, h, i = rng.uniform(-20, 20, 3)
+            d, e, f = rng.uniform(-1.5, 1.5, 3) if cross else (0, 0, 0)
             lines.append(f"quadric, diffuse_color: [{dif}], specular_color: [{spe}], a: {a:.2f}, "
-                         f"b: {b:.2f}, c: {c:.2f}, d: 0, e: 0, f: 0, g: {g:.2f}, h: {h:.2f}, "
+                         f"b: {b:.2f}, c: {c:.2f}, d: {d:.2f}, e: {e:.2f}, f: {f:.2f}, "
+                         f"g: {g:.2f}, h: {h:.2f}, "
                          f"i: {i:.2f}, j: {rng.uniform(50, 300):.2f}, reflectivity: {refl:.3f}")
     for k in range(n_lights):
         col = rng.uniform(0.6, 4, 3)

@@ -7,8 +7,8 @@ import subprocess
 import numpy as np
 import pytest
 
-from helpers import (GOLDEN, ROOT, file_md5, golden_key, golden_table, oracle_render, p3_md5,
-                     random_scene, rc, scene_path)
+from helpers import (GOLDEN, ROOT, file_md5, golden_key, golden_table, oracle_lib, oracle_render,
+                     p3_md5, random_scene, rc, scene_path)
 
 pytestmark = pytest.mark.gpu
 
@@ -67,6 +67,7 @@ SCHEDULES = {"no-side": dict(side=0), "side-always": dict(side=1), "side-by-size
              "resolve-shared": dict(resolve_shared=1), "no-dep-fast": dict(dep_fast=0),
              "no-side+no-dep-fast": dict(side=0, dep_fast=0),
              "no-side+phase-c-finish": dict(side=0, phase_c_finish=1), "no-o0": dict(o0=0),
+             "no-x0": dict(x0=0),
              "hand-run-1": dict(hand_run=1), "helpers-1": dict(helpers=1),
              "no-helpers": dict(helpers=0), "no-coop": dict(coop=0),
              "small-grid": dict(resolve_grid=64, team_blocks=16),
@@ -82,7 +83,8 @@ def test_parity_schedules(sched, scenes, table):
     the resolver (split_shade), no one-workgroup-per-CU reservation (resolve_shared, which
     also disables the side stream), every first-bounce-miss pixel recomputed in phase C
     (dep_fast=0), primary rays through the general intersection tests instead of the origin-
-    zero forms (o0=0), a hand-off to the helper blocks after every change (hand_run=1: the
+    zero forms (o0=0), the quadric tests with their cross terms although they are zero (x0=0),
+    a hand-off to the helper blocks after every change (hand_run=1: the
     queue overflows), a single helper block, none, the lane-only evaluator (coop=0), a small
     resolver grid, and the plain serial copy to the host."""
     with rc.tuned(**SCHEDULES[sched]):
@@ -116,6 +118,68 @@ ZERO_EVENT_PLANES = [((0, 0, 1), 0.5, ""), ((0, 0.6, 0.8), 0.5, ""), ((0, 0.28, 
                      ((0.6, 0, 0.8), 0.4, "sphere, radius: 1.0, diffuse_color: [1, 0, 0], "
                       "specular_color: [1, 1, 1], position: [0, 3, -2], reflectivity: 0.5, "
                       "refractivity: 0.0, ior: 1.0\n")]
+
+
+@pytest.mark.parametrize("x0", [1, 0])
+@pytest.mark.parametrize("cross", [False, True])
+def test_quadric_cross_terms_vs_oracle(cross, x0, tmp_path):
+    """Quadrics with and without cross coefficients d, e, f (C/raycast.c:614-656).  Without
+    them (every example scene) the kernels drop the cross terms (rc_device.hpp quad_abc,
+    rc_tuning.x0); with them, or with x0 = 0, the full accumulations run.  Against the CPU
+    oracle, both modes, every depth class, one frame at a time."""
+    rng = np.random.default_rng(77 + int(cross))
+    path = str(tmp_path / f"q{int(cross)}.scene")
+    random_scene(rng, path, 14, 2, cross=cross)
+    s = rc.Scene.from_file(path)
+    with rc.tuned(x0=x0):
+        for mode in ("parity", "fast"):
+            for d in (1, 4, 6):
+                want, st = oracle_render(s, 96, 72, d, mode)
+                if not st["parity_defined"]:
+                    continue
+                np.testing.assert_array_equal(rc.render(s, 96, 72, depth=d, mode=mode), want,
+                                              err_msg=f"cross={cross} x0={x0} {mode} d{d}")
+
+
+CROSS_NAN_QUADRICS = (
+    "quadric, diffuse_color: [1.0, 0.5, 0], a: 0, b: 1, c: 1, d: 0, e: 0, f: 0, g: 0, h: -10, "
+    "i: 20, j: 124, reflectivity: 0.2\n"
+    "quadric, diffuse_color: [0, 0.5, 1.0], specular_color: [0.5, 0.5, 0.5], a: 1, b: 0, c: 1, "
+    "d: 0, e: 0, f: 0, g: 4, h: 0, i: 10, j: 28, reflectivity: 0.3\n")
+
+
+@pytest.mark.parametrize("cam,y", [(20, "1.2e38"), (2000, "1.5e38")])
+def test_cross_term_nan_rejection(cam, y, tmp_path):
+    """Hit points beyond float range: two mirror planes at y = -+1.2e38 (or 1.5e38) send the
+    second bounce's hit point to +-inf, where the reference's zero cross terms of a quadric
+    test become NaN (0 * inf) and reject the quadric.  The kernels' cross-term-free form
+    reproduces that through x0_reject (rc_device.hpp); the oracle's diagnostic counter shows
+    the case is exercised.  Parity and fast mode, x0 on and off, against the oracle."""
+    path = tmp_path / "xnan.scene"
+    path.write_text(
+        f"camera, width: {cam}, height: {cam}\n" + CROSS_NAN_QUADRICS +
+        f"plane, normal: [0, 1, 0], diffuse_color: [0.3, 0.3, 0.3], position: [0, -{y}, 0], "
+        "reflectivity: 1.0\n"
+        f"plane, normal: [0, -1, 0], diffuse_color: [0.3, 0.6, 0.3], position: [0, {y}, 0], "
+        "reflectivity: 1.0\n"
+        "sphere, radius: 1.0, diffuse_color: [0.2, 0.2, 1], specular_color: [1, 1, 1], "
+        "position: [2, 0, -7], reflectivity: 0.5, refractivity: 0, ior: 1\n"
+        "light, color: [2, 2, 2], radial-a2: 0.01, radial-a1: 0.0125, radial-a0: 0.0125, "
+        "position: [1, 3, -2]\n")
+    s = rc.Scene.from_file(str(path))
+    lib = oracle_lib()
+    for x0 in (1, 0):
+        with rc.tuned(x0=x0):
+            for mode in ("parity", "fast"):
+                for w, h, d in ((64, 48, 6), (7, 5, 4)):
+                    lib.rco_cross_nan_events(1)
+                    want, st = oracle_render(s, w, h, d, mode)
+                    if w == 64:
+                        assert lib.rco_cross_nan_events(1) > 0, "the NaN cross-term case is not hit"
+                    if not st["parity_defined"]:
+                        continue
+                    np.testing.assert_array_equal(rc.render(s, w, h, depth=d, mode=mode), want,
+                                                  err_msg=f"x0={x0} {mode} {w}x{h} d{d}")
 
 
 @pytest.mark.parametrize("case", range(len(ZERO_EVENT_PLANES)))
