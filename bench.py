@@ -82,7 +82,7 @@ PMC_PROFILES = {("quadric", 4096, 6, "parity"): "profiles/r03e_pmc_lone_4096.jso
 # FETCH/WRITE of the frames-in-flight launches themselves (scripts/pmc_traffic.py over the
 # bench's timed launches): a pipeline lane's resolver has no phase C inside, so its traffic
 # differs from the lone frame's
-PMC_TRAFFIC_INFLIGHT = {("quadric", 4096, 6, "parity"): "profiles/r03e_pmc_traffic_inflight_4096.json"}
+PMC_TRAFFIC_INFLIGHT = {("quadric", 4096, 6, "parity"): "profiles/r03f_pmc_traffic_inflight_4096.json"}
 
 
 def pmc_kernel(kernel, scene, size, depth, mode, inflight=False):

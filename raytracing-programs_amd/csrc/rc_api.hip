@@ -376,7 +376,7 @@ int rc_set_tuning(const rc_tuning* t) {
       in(t->pipe_timing, 0, 1) && in(t->pipe_slotstreams, 0, 1) && in(t->overlap_d2h, 0, 1) &&
       in(t->staged_d2h, 0, 1) && in(t->prefault, 0, 1) && in(t->copy_threads, 1, 32) &&
       in(t->comp_stream, 0, 2) && in(t->side_blocks, 0, 1 << 16) &&
-      in(t->block_min, 0, 1 << 30) && in(t->pipe_inres, 0, 2) &&
+      in(t->block_min, 0, 1 << 30) && in(t->pipe_inres, 0, 2) && in(t->x0, 0, 1) &&
       !(t->split_shade && !t->side);
   if (!ok) {
     std::fprintf(stderr, "Error: rc_set_tuning: a field is out of range\n");

@@ -219,7 +219,7 @@ def test_tuning_api_validates():
     assert rc.get_tuning() == base
     for bad in (dict(pipe_resolvers=0), dict(pipe_resolvers=5), dict(helpers=65),
                 dict(team_blocks=-2), dict(resolve_grid=4), dict(split_shade=1, side=0),
-                dict(copy_threads=0), dict(resolve_lds_kb=200), dict(long_len=10)):
+                dict(copy_threads=0), dict(resolve_lds_kb=200), dict(long_len=10), dict(x0=2)):
         with pytest.raises(ValueError):
             rc.set_tuning(**bad)
         assert rc.get_tuning() == base, bad
