@@ -1145,8 +1145,10 @@ __device__ __forceinline__ V3 carry_path_spec(const Scene& sc, const LaneShape& 
     float tt = 0.0f;
     // kQ = 2: quadrics without cross terms, rejected where a cross term would be NaN
     // (quad_abc, x0_reject)
-    const bool tok = test_unified<kQuad, kQ == 2>(ls.s, C, myD, rk, myS, tt) &&
-                     !(kQ == 2 && ls.s.type == RC_SHAPE_QUADRIC && x0_reject(C, myD));
+    // (bitwise, not short-circuit: a branch here would split the step's basic block)
+    bool rejq = false;
+    if constexpr (kQ == 2) rejq = (ls.s.type == RC_SHAPE_QUADRIC) & x0_reject(C, myD);
+    const bool tok = test_unified<kQuad, kQ == 2>(ls.s, C, myD, rk, myS, tt) & !rejq;
     const bool ok = tok && ls.has && kself != myS && __builtin_inff() > tt && tt > 0.0f;
     float t = ok ? tt : __builtin_inff();
     int k = ok ? kself : kNone;
