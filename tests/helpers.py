@@ -226,3 +226,22 @@ def phantom_lit_scene(path, kind):
     with open(path, "w") as f:
         f.write(text.replace(QUADRIC_POINT_LIGHT, PHANTOM_LIT[kind]) + "\n")
     return path
+
+
+def cross_nan_scene_text(cam, y):
+    """Two mirror planes at y = -+Y (Y ~ 1e38) beside the quadric example's cross-term-free
+    quadrics: second-bounce hit points overflow to inf, where the reference's zero cross terms
+    become NaN (0 * inf) and reject the quadric (rc_device.hpp x0_reject)."""
+    return (f"camera, width: {cam}, height: {cam}\n"
+            "quadric, diffuse_color: [1.0, 0.5, 0], a: 0, b: 1, c: 1, d: 0, e: 0, f: 0, g: 0, "
+            "h: -10, i: 20, j: 124, reflectivity: 0.2\n"
+            "quadric, diffuse_color: [0, 0.5, 1.0], specular_color: [0.5, 0.5, 0.5], a: 1, b: 0, "
+            "c: 1, d: 0, e: 0, f: 0, g: 4, h: 0, i: 10, j: 28, reflectivity: 0.3\n"
+            f"plane, normal: [0, 1, 0], diffuse_color: [0.3, 0.3, 0.3], position: [0, -{y}, 0], "
+            "reflectivity: 1.0\n"
+            f"plane, normal: [0, -1, 0], diffuse_color: [0.3, 0.6, 0.3], position: [0, {y}, 0], "
+            "reflectivity: 1.0\n"
+            "sphere, radius: 1.0, diffuse_color: [0.2, 0.2, 1], specular_color: [1, 1, 1], "
+            "position: [2, 0, -7], reflectivity: 0.5, refractivity: 0, ior: 1\n"
+            "light, color: [2, 2, 2], radial-a2: 0.01, radial-a1: 0.0125, radial-a0: 0.0125, "
+            "position: [1, 3, -2]\n")

@@ -7,8 +7,8 @@ import subprocess
 import numpy as np
 import pytest
 
-from helpers import (GOLDEN, ROOT, file_md5, golden_key, golden_table, oracle_lib, oracle_render,
-                     p3_md5, random_scene, rc, scene_path)
+from helpers import (GOLDEN, ROOT, cross_nan_scene_text, file_md5, golden_key, golden_table,
+                     oracle_lib, oracle_render, p3_md5, random_scene, rc, scene_path)
 
 pytestmark = pytest.mark.gpu
 
@@ -141,13 +141,6 @@ def test_quadric_cross_terms_vs_oracle(cross, x0, tmp_path):
                                               err_msg=f"cross={cross} x0={x0} {mode} d{d}")
 
 
-CROSS_NAN_QUADRICS = (
-    "quadric, diffuse_color: [1.0, 0.5, 0], a: 0, b: 1, c: 1, d: 0, e: 0, f: 0, g: 0, h: -10, "
-    "i: 20, j: 124, reflectivity: 0.2\n"
-    "quadric, diffuse_color: [0, 0.5, 1.0], specular_color: [0.5, 0.5, 0.5], a: 1, b: 0, c: 1, "
-    "d: 0, e: 0, f: 0, g: 4, h: 0, i: 10, j: 28, reflectivity: 0.3\n")
-
-
 @pytest.mark.parametrize("cam,y", [(20, "1.2e38"), (2000, "1.5e38")])
 def test_cross_term_nan_rejection(cam, y, tmp_path):
     """Hit points beyond float range: two mirror planes at y = -+1.2e38 (or 1.5e38) send the
@@ -156,16 +149,7 @@ def test_cross_term_nan_rejection(cam, y, tmp_path):
     reproduces that through x0_reject (rc_device.hpp); the oracle's diagnostic counter shows
     the case is exercised.  Parity and fast mode, x0 on and off, against the oracle."""
     path = tmp_path / "xnan.scene"
-    path.write_text(
-        f"camera, width: {cam}, height: {cam}\n" + CROSS_NAN_QUADRICS +
-        f"plane, normal: [0, 1, 0], diffuse_color: [0.3, 0.3, 0.3], position: [0, -{y}, 0], "
-        "reflectivity: 1.0\n"
-        f"plane, normal: [0, -1, 0], diffuse_color: [0.3, 0.6, 0.3], position: [0, {y}, 0], "
-        "reflectivity: 1.0\n"
-        "sphere, radius: 1.0, diffuse_color: [0.2, 0.2, 1], specular_color: [1, 1, 1], "
-        "position: [2, 0, -7], reflectivity: 0.5, refractivity: 0, ior: 1\n"
-        "light, color: [2, 2, 2], radial-a2: 0.01, radial-a1: 0.0125, radial-a0: 0.0125, "
-        "position: [1, 3, -2]\n")
+    path.write_text(cross_nan_scene_text(cam, y))
     s = rc.Scene.from_file(str(path))
     lib = oracle_lib()
     for x0 in (1, 0):

@@ -11,8 +11,9 @@ import os
 import numpy as np
 import pytest
 
-from helpers import (GOLDEN, PHANTOM_LIT, SCENES, golden_key, golden_table, have_ref, oracle_render, p3_md5, phantom_lit_scene,
-                     rc, run_ref, scene_path, random_scene)
+from helpers import (GOLDEN, PHANTOM_LIT, SCENES, cross_nan_scene_text, golden_key, golden_table,
+                     have_ref, oracle_lib, oracle_render, p3_md5, phantom_lit_scene, rc, run_ref,
+                     scene_path, random_scene)
 
 SMALL = ["simple", "reflection", "quadric", "example2", "example3", "quadric2"]
 
@@ -82,6 +83,32 @@ def test_oracle_vs_reference_random_scenes(seed, tmp_path):
             if not st["parity_defined"]:
                 continue
             np.testing.assert_array_equal(img, run_ref(path, 48, 40, d, mode))
+
+
+@pytest.mark.skipif(not have_ref(), reason="oracle/_ref not built (make ref)")
+@pytest.mark.parametrize("case", ["cross-terms", "overflow-1.2e38", "overflow-1.5e38"])
+def test_oracle_vs_reference_quadric_cross_terms(case, tmp_path):
+    """Pins the oracle where the kernels' cross-term-free quadric form must agree with the
+    reference: quadrics with non-zero d, e, f, and hit points that overflow to inf so that
+    the zero cross terms turn NaN (the oracle's diagnostic counter shows that case is hit)."""
+    path = tmp_path / f"{case}.scene"
+    if case == "cross-terms":
+        random_scene(np.random.default_rng(78), str(path), 14, 2, cross=True)
+        w, h = 48, 40
+    else:
+        path.write_text(cross_nan_scene_text(20 if "1.2" in case else 2000, case.split("-")[1]))
+        w, h = 64, 48
+    s = rc.Scene.from_file(str(path))
+    lib = oracle_lib()
+    for mode in ("parity", "fast"):
+        for d in (1, 6):
+            lib.rco_cross_nan_events(1)
+            img, st = oracle_render(s, w, h, d, mode)
+            if case != "cross-terms" and d == 6:
+                assert lib.rco_cross_nan_events(1) > 0
+            if st["parity_defined"]:
+                np.testing.assert_array_equal(img, run_ref(str(path), w, h, d, mode),
+                                              err_msg=f"{case} {mode} d{d}")
 
 
 @pytest.mark.skipif(not have_ref(), reason="oracle/_ref not built (make ref)")
