@@ -282,6 +282,11 @@ typedef struct rc_tuning {
                              lane's own resolver work is over (k_finish shades the rest)     */
   int x0;                 /* 1: quadrics whose d, e, f are all zero are tested without their
                              cross terms (bit-identical, rc_device.hpp quad_abc; default 1) */
+  int resolve_clean;      /* clean 256-entry windows in a row before the team leader hands a
+                             RESOLVE round back to the team's SCAN (1..64)                   */
+  int shard_lone;         /* 1: a one-rank group renders its image as a lone frame (default);
+                             0: through the sharded exchange (wire records, gathers, the
+                             root's resolver) like a multi-rank group — test and measurement */
 } rc_tuning;
 void rc_default_tuning(rc_tuning *t);
 int rc_set_tuning(const rc_tuning *t);

@@ -97,7 +97,8 @@ TUNING_FIELDS = ["side", "split_shade", "resolve_shared", "resolve_lds_kb", "res
                  "dep_fast", "o0", "phase_c_finish", "single_res_cus", "pipe_res_cus",
                  "pipe_resolvers", "pipe_slots", "pipe_timing", "pipe_slotstreams", "overlap_d2h",
                  "staged_d2h", "prefault", "copy_threads", "side_blocks", "comp_stream",
-                 "block_min", "pipe_inres", "x0"]
+                 "block_min", "pipe_inres", "x0", "resolve_clean",
+                 "shard_lone"]
 
 
 class RcTuning(ctypes.Structure):

@@ -65,6 +65,8 @@ rc_tuning default_tuning() {
   t.comp_stream = 2;
   t.pipe_inres = 0;
   t.x0 = 1;
+  t.resolve_clean = 1;
+  t.shard_lone = 1;
   // regular segments of >= 3000 entries on whole workgroups when there are workgroups for all
   // of them (k_seg_order): lone quadric 4096^2 5.19 -> 5.06 ms (its ~100 3856-entry segments
   // 4.4 -> 2.5 ms, under the team segment); 8192^2 and pipeline lanes have more such segments
@@ -144,6 +146,17 @@ long long FrameLog::drain() {
     tail = head;
   }
   return found;
+}
+
+bool FrameLog::earlier_failed() {
+  poll();
+  return failed > 0;
+}
+
+bool FrameLog::entry_failed(long long k) const {
+  if (!ring || k < tail || k >= head) return false;   // not logged, or already read back
+  const int code = ((volatile const Entry*)&ring[k % kRing])->code;
+  return code != 0 && code != kPending;
 }
 
 void FrameLog::take(long long* c, long long* f) {
@@ -377,6 +390,7 @@ int rc_set_tuning(const rc_tuning* t) {
       in(t->staged_d2h, 0, 1) && in(t->prefault, 0, 1) && in(t->copy_threads, 1, 32) &&
       in(t->comp_stream, 0, 2) && in(t->side_blocks, 0, 1 << 16) &&
       in(t->block_min, 0, 1 << 30) && in(t->pipe_inres, 0, 2) && in(t->x0, 0, 1) &&
+      in(t->resolve_clean, 1, 64) && in(t->shard_lone, 0, 1) &&
       !(t->split_shade && !t->side);
   if (!ok) {
     std::fprintf(stderr, "Error: rc_set_tuning: a field is out of range\n");
@@ -631,6 +645,7 @@ int ensure_parity(DevCtx& c, FrameBufs& b, int W, int H, rc::ParityWork& w, int 
   w.block_min = tu.block_min;
   w.wave_k = tu.wave_k;
   w.resolve_k = tu.resolve_k;
+  w.resolve_clean = tu.resolve_clean;
   w.coop_group = 0;
   if (tu.coop && b.scene_src) {
     const int n = ((const rc_packed_header*)b.scene_src)->n;
@@ -930,11 +945,12 @@ int rc_render_device(const rc_scene* s, int W, int H, int row0, int row_step, in
   std::lock_guard<std::mutex> lk(c->mu);
   // an earlier frame of this workspace whose hand-off failed is reported by the next call
   // (once: the report consumes the counts)
-  if (c->lone_log.poll() > 0) {
+  if (c->lone_log.earlier_failed()) {
     c->lone_log.take(nullptr, nullptr);
     return -1;
   }
   hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+  const long long own = c->lone_log.head;   // this frame's ring entry (parity frames log one)
   // the scene upload and events live on the ctx stream: order them with the caller's stream
   if (st != c->stream) {
     hipStream_t saved = c->stream;
@@ -949,7 +965,9 @@ int rc_render_device(const rc_scene* s, int W, int H, int row0, int row_step, in
     std::memset(timing, 0, sizeof *timing);
     HIP_TRY(hipStreamSynchronize(st));
     const long long before = c->lone_log.checked;
-    if (c->lone_log.poll() > 0) {
+    const bool failed = c->lone_log.entry_failed(own);
+    c->lone_log.poll();
+    if (failed) {
       c->lone_log.take(nullptr, nullptr);
       return -1;
     }
@@ -1215,8 +1233,10 @@ int rc_lone_frames_check(int64_t* checked, int64_t* failed) {
   HIP_TRY(hipGetDevice(&dev));
   DevCtx* c;
   if (ctx_get(dev, &c)) return -1;
-  HIP_TRY(hipDeviceSynchronize());   // the frames ran on the callers' streams
+  // the lock first: a frame another thread enqueues after the synchronisation would otherwise
+  // be drained while still pending (counted as never verified)
   std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(hipDeviceSynchronize());   // the frames ran on the callers' streams
   c->lone_log.drain();
   long long ch = 0, f = 0;
   c->lone_log.take(&ch, &f);
@@ -1324,6 +1344,12 @@ int rc_render(const rc_scene* s, int W, int H, const rc_options* opt, uint8_t* p
   // the lock covers the workspace from its (re)allocation on: a concurrent caller's ensure()
   // could otherwise free the buffer another caller is rendering into
   std::lock_guard<std::mutex> lk(c->mu);
+  // an earlier frame's failure (rc_render_device on another stream) is reported before this
+  // frame is enqueued, as rc_render_device does, so the result below is this frame's own
+  if (c->lone_log.earlier_failed()) {
+    c->lone_log.take(nullptr, nullptr);
+    return -1;
+  }
   if (c->out.ensure((size_t)H * row_bytes)) return -1;
   uint8_t* d_out = (uint8_t*)c->out.p;
   // parity: the copy overlaps the resolver (copy_overlapped); split shading leaves the non-DEP
@@ -1337,6 +1363,7 @@ int rc_render(const rc_scene* s, int W, int H, const rc_options* opt, uint8_t* p
     patch = (uint32_t*)c->patch.p;
   }
   hipEvent_t* ev = nullptr;
+  const long long own = c->lone_log.head;   // this frame's ring entry (parity frames log one)
   if (enqueue_render(*c, s, W, H, 0, 1, H, opt, d_out, c->stream, true, patch, &ev)) return -1;
   prefault(pixmap, (size_t)H * row_bytes);
   auto td = std::chrono::steady_clock::now();
@@ -1345,14 +1372,16 @@ int rc_render(const rc_scene* s, int W, int H, const rc_options* opt, uint8_t* p
   } else if (copy_to_host(*c, pixmap, d_out, (size_t)H * row_bytes, c->stream)) {
     return -1;
   }
-  // this frame's latched hand-off words (and any earlier frame's still unread); a failure is
-  // reported by this call and consumed
+  // this frame's latched hand-off words: its own failure is reported by this call and
+  // consumed; another stream's frame that failed meanwhile is left to the next call
   HIP_TRY(hipStreamSynchronize(c->stream));
-  if (c->lone_log.poll() > 0) {
+  if (c->lone_log.entry_failed(own)) {
+    c->lone_log.poll();
     (void)check_spin_error(c->fb, opt);   // the details, while the workspace still holds them
     c->lone_log.take(nullptr, nullptr);
     return -1;
   }
+  c->lone_log.poll();
   if (timing) {
     fill_device_timing(*c, opt, timing);
     timing->d2h_ms =

@@ -77,6 +77,32 @@ __device__ __forceinline__ float dot(V3 a, V3 b) {
 }
 __device__ __forceinline__ V3 sub(V3 a, V3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
 
+// Quotients n / d of the resolver's shape test through one shared reciprocal.  This is the
+// compiler's IEEE f64 division sequence (v_rcp_f64, two Newton steps, q0 = n*y, the residual
+// r = n - d*q0 and q = q0 + r*y, each rounded once) without its v_div_scale / v_div_fmas /
+// v_div_fixup steps, which change nothing unless an operand is extreme: they rescale only for
+// |n| < 2^-969, |d| > 2^1021 or exponent gaps beyond 768, and fix up zero, inf and NaN
+// operands.  The tests' operands are float-derived (|n| in [2^-201, 2^130] or 0, |d| in
+// [2^-148, 2^130]), so every finite quotient is bit-identical to n / d; where n or d is 0, inf
+// or NaN the value differs (NaN or an unsigned zero instead of +-inf or -0) but such a t is
+// rejected either way (t > 0 and t < inf; a zero or infinite denominator never yields an
+// accepted root), which is all the callers use it for.
+#ifndef RC_NRDIV
+#define RC_NRDIV 1
+#endif
+__device__ __forceinline__ double recip_nr(double d) {
+  double y = __builtin_amdgcn_rcp(d);
+  double e = __builtin_fma(-d, y, 1.0);
+  y = __builtin_fma(y, e, y);
+  e = __builtin_fma(-d, y, 1.0);
+  return __builtin_fma(y, e, y);
+}
+__device__ __forceinline__ double div_nr(double n, double d, double y) {
+  const double q0 = n * y;
+  const double r = __builtin_fma(-d, q0, n);
+  return __builtin_fma(r, y, q0);
+}
+
 // Correctly rounded f64 sqrt for s = +-0, s >= 2^-767, +inf or NaN — every value it is used
 // on here: sums of squares of floats (0 or >= 2^-298) and non-negative floats widened to
 // double (0 or >= 2^-149).  This is the compiler's own rsq + Goldschmidt/Newton sequence
@@ -220,10 +246,24 @@ __device__ __forceinline__ double pown_dd(double a, int n) {
 struct RayK {
   float a4;     // 4 * a               (float, C/raycast.c:587)
   double den;   // 2.0 * (double)a     (C/raycast.c:593)
+  double yden;  // recip_nr(den): the sphere quotients' shared reciprocal (RC_NRDIV)
 };
 __device__ __forceinline__ RayK ray_consts(V3 D) {
   float a = (float)sumsq3((double)D.x, (double)D.y, (double)D.z);
-  return RayK{4.0f * a, 2.0 * (double)a};
+  const double den = 2.0 * (double)a;
+  return RayK{4.0f * a, den, RC_NRDIV ? recip_nr(den) : 0.0};
+}
+
+// The candidate t = (float)(num / den) of a shape test (accepted only when 0 < t < inf):
+// through the shared reciprocal y = recip_nr(den) (RC_NRDIV; bit-identical for every finite
+// quotient, a rejected t for zero, infinite or NaN operands either way), else as written.
+__device__ __forceinline__ float tquot(double num, double den, double y) {
+#if RC_NRDIV
+  return (float)div_nr(num, den, y);
+#else
+  (void)y;
+  return (float)(num / den);
+#endif
 }
 
 // C/raycast.c:576-600
@@ -235,9 +275,11 @@ __device__ __forceinline__ bool hit_sphere(V3 O, V3 D, const rc_shape& s, RayK k
   float disc = (float)__builtin_fma((double)b, (double)b, -(double)fac);
   if (disc < 0.0f) return false;
   double sq = sqrt_ns((double)disc);
-  float tt = (float)(((double)(-b) - sq) / k.den);
-  if (tt < 0.0f) tt = (float)(((double)(-b) + sq) / k.den);
-  t = tt;
+  // both roots, then a select (with the shared reciprocal the second costs three operations,
+  // less than the branch around it)
+  const float t1 = pin(tquot((double)(-b) - sq, k.den, k.yden));
+  const float t2 = pin(tquot((double)(-b) + sq, k.den, k.yden));
+  t = t1 < 0.0f ? t2 : t1;
   return true;
 }
 
@@ -328,16 +370,17 @@ __device__ __forceinline__ bool hit_quadric(V3 O, V3 D, const rc_shape& q, float
   quad_abc(O, D, q, aq, bq, cq, x0);
   if (rej) return false;
   if ((double)aq == 0.0) {
-    t = (float)((-1.0 * (double)cq) / (double)bq);
+    t = tquot(-1.0 * (double)cq, (double)bq, RC_NRDIV ? recip_nr((double)bq) : 0.0);
     return true;
   }
   const float disc = (float)__builtin_fma((double)bq, (double)bq, -(4.0 * (double)aq * (double)cq));
   if ((double)disc < 0.0) return false;
   const double den = 2.0 * (double)aq;
   const double sq = sqrt_ns((double)disc);
-  float tt = (float)(((double)(-bq) - sq) / den);
-  if (tt <= 0.0f) tt = (float)(((double)(-bq) + sq) / den);
-  t = tt;
+  const double y = RC_NRDIV ? recip_nr(den) : 0.0;
+  const float t1 = pin(tquot((double)(-bq) - sq, den, y));
+  const float t2 = pin(tquot((double)(-bq) + sq, den, y));
+  t = t1 <= 0.0f ? t2 : t1;
   return true;
 }
 
@@ -390,9 +433,9 @@ __device__ __forceinline__ bool hit_sphere_o0(V3 D, const rc_shape& s, RayK k, f
   float disc = (float)__builtin_fma((double)b, (double)b, -(double)fac);
   if (disc < 0.0f) return false;
   double sq = sqrt_ns((double)disc);
-  float tt = (float)(((double)(-b) - sq) / k.den);
-  if (tt < 0.0f) tt = (float)(((double)(-b) + sq) / k.den);
-  t = tt;
+  const float t1 = pin(tquot((double)(-b) - sq, k.den, k.yden));
+  const float t2 = pin(tquot((double)(-b) + sq, k.den, k.yden));
+  t = t1 < 0.0f ? t2 : t1;
   return true;
 }
 
@@ -422,16 +465,17 @@ __device__ __forceinline__ bool hit_quadric_o0(V3 D, const rc_shape& q, float& t
   const float bq = (float)acc;
   const float cq = q.o0;
   if ((double)aq == 0.0) {
-    t = (float)((-1.0 * (double)cq) / (double)bq);
+    t = tquot(-1.0 * (double)cq, (double)bq, RC_NRDIV ? recip_nr((double)bq) : 0.0);
     return true;
   }
   const float disc = (float)__builtin_fma((double)bq, (double)bq, -(4.0 * (double)aq * (double)cq));
   if ((double)disc < 0.0) return false;
   const double den = 2.0 * (double)aq;
   const double sq = sqrt_ns((double)disc);
-  float tt = (float)(((double)(-bq) - sq) / den);
-  if (tt <= 0.0f) tt = (float)(((double)(-bq) + sq) / den);
-  t = tt;
+  const double y = RC_NRDIV ? recip_nr(den) : 0.0;
+  const float t1 = pin(tquot((double)(-bq) - sq, den, y));
+  const float t2 = pin(tquot((double)(-bq) + sq, den, y));
+  t = t1 <= 0.0f ? t2 : t1;
   return true;
 }
 
@@ -524,7 +568,7 @@ __device__ __forceinline__ bool shadow_quadric(V3 O, V3 D, const rc_shape& q, in
   }
   if (cls != kQPos) return false;
   if (skip != -1 && D.z < 0.0f) {
-    const float t = (float)(num / den);
+    const float t = tquot(num, den, RC_NRDIV ? recip_nr(den) : 0.0);   // a positive finite t (cls)
     if ((O.z + t * D.z) < O.z) return false;
   }
   return true;
@@ -1056,8 +1100,14 @@ __device__ __forceinline__ bool test_unified(const rc_shape& s, V3 O, V3 D, RayK
   const double den1 =
       isP ? (double)denP : (qlin ? (double)bq : ((isS || !kQuad) ? rk.den : 2.0 * (double)aq));
   const double num2 = nb + sq;
+#if RC_NRDIV
+  const double y1 = recip_nr(den1);
+  const float q1 = (float)pin(div_nr(num1, den1, y1));
+  const float q2 = (float)pin(div_nr(num2, den1, y1));
+#else
   const float q1 = (float)pin(num1 / den1);
   const float q2 = (float)pin(num2 / den1);
+#endif
   // sphere: second root if the first is negative; quadric: if it is not positive
   const bool second = (isS & (q1 < 0.0f)) | (isQ & !lin & (q1 <= 0.0f));
   const float tt = second ? q2 : q1;
@@ -1112,6 +1162,9 @@ __device__ __forceinline__ void hit_frame_sel(const rc_shape& s, V3 O, V3 D, flo
 // so the scheduler can overlap the independent chains of a lone wave.  GT = the group size
 // as a compile-time constant (4, 8, 16), or 0 for the runtime value Grt; kQ = 0: the scene has
 // no quadric, 1: it has, 2: none of its quadrics has cross terms (quad_x0, quad_abc).
+#ifndef RC_LAST_SKIP
+#define RC_LAST_SKIP 0   // measured: lone resolver 4.21 -> 4.37 ms (the branch splits the step)
+#endif
 template <int GT, int kQ>
 __device__ __forceinline__ V3 carry_path_spec(const Scene& sc, const LaneShape& ls, int kself,
                                               int Grt, int half, const DepRec& r, int maxrec,
@@ -1177,6 +1230,19 @@ __device__ __forceinline__ V3 carry_path_spec(const Scene& sc, const LaneShape& 
     const V3 Dw = sel(two, D2, D1);
     const bool hit = w != kNone;
     anyhit = anyhit | hit;
+#if RC_LAST_SKIP
+    // Every path of the wave ends at this level (the last level, or a non-reflective object):
+    // the carry is the hit point alone, so the normal and its normalisation are skipped (a
+    // wave-uniform branch; a changer's last level costs ~75 instructions less).
+    {
+      const int lnext = lvl + (two ? 2 : 1);
+      const bool last = lnext >= maxrec || !reflective(sc, hit ? w : obj);
+      if (__ballot(!last) == 0) {
+        C = sel(hit, v3(C.x + Dw.x * tw, C.y + Dw.y * tw, C.z + Dw.z * tw), C);
+        break;
+      }
+    }
+#endif
     V3 P, Nw;
     hit_frame_sel<kQuad>(sc.shapes[hit ? w : 0], C, Dw, tw, P, Nw);
     C = sel(hit, P, C);

@@ -58,6 +58,7 @@ struct ParityWork {
   int phase_c_finish;       // phase C after the resolver through k_finish's claims (RC_PHASE_C_FINISH)
   int wave_k;               // clean cooperative steps before a wave window goes back to LANE
   int resolve_k;            // the same for the team leader's block window
+  int resolve_clean;        // clean windows in a row that end a RESOLVE round
   int coop_group;           // lanes per entry of the cooperative evaluator (0: off)
   unsigned* trace;          // optional [2*nseg] per-segment {ticks, evals} (debug)
   // Pipelined frames (rc_frame_submit): the resolver runs on its own stream (a CU partition

@@ -1713,7 +1713,7 @@ __global__ void __launch_bounds__(kResolveBlock) __attribute__((amdgpu_waves_per
     const int* __restrict__ seg_start, const int* __restrict__ seg_order,
     int* __restrict__ counters, int* __restrict__ head,
     CinG* __restrict__ cin, int team_blocks, int long_len, TeamState* __restrict__ ts,
-    unsigned* __restrict__ trace, int G, int wave_k, int resolve_k, unsigned tag,
+    unsigned* __restrict__ trace, int G, int wave_k, int resolve_k, int resolve_clean, unsigned tag,
     int helpers, int hand_run, int inject, int block_min, int* __restrict__ rq_cnt,
     int* __restrict__ rq, Cam cam, int W, uint8_t* __restrict__ out, uint32_t* __restrict__ patch,
     unsigned long long* __restrict__ zcount, int* __restrict__ batch_state, int inres) {
@@ -1911,6 +1911,7 @@ __global__ void __launch_bounds__(kResolveBlock) __attribute__((amdgpu_waves_per
           // ------------------------------------------------------------- RESOLVE
           if (blockIdx.x == 0) {
             bool dense = true;   // the cluster starts right after a changer
+            int clean = 0;       // clean windows in a row (resolve_clean of them end the round)
             // records of the first window; later windows are prefetched one ahead
             const int t = threadIdx.x;
             if (j + t < end) s_bw.rec[t] = rec_at(deprec, dep_pix, j + t);
@@ -1925,7 +1926,11 @@ __global__ void __launch_bounds__(kResolveBlock) __attribute__((amdgpu_waves_per
                            tag, tws);
               j = jn;
               __syncthreads();   // everyone is done reading this window's records
-              if (!changed) break;   // a clean window: the cluster is over
+              // resolve_clean clean windows in a row: the cluster is over (the next one is
+              // the team's to find; a short gap costs a LANE pass here instead of a SCAN round
+              // and two hand-offs)
+              clean = changed ? 0 : clean + 1;
+              if (clean >= resolve_clean) break;
               if (j + t < end) s_bw.rec[t] = nxt;
               __syncthreads();
             }
@@ -2744,7 +2749,7 @@ hipError_t launch_parity(const LaunchScene& s, int W, int H, int maxrec, uint8_t
                      maxrec, (const DepRec*)w.deprec, w.dep_pix, w.seg_key, w.wcarry,
                      w.seg_start, w.seg_order, w.counters, w.counters + 1, (CinG*)w.cin, w.team_blocks,
                      w.long_len, (TeamState*)w.team, w.trace, w.coop_group, w.wave_k,
-                     w.resolve_k, w.epoch, w.helpers, w.hand_run, w.inject, w.block_min,
+                     w.resolve_k, w.resolve_clean > 0 ? w.resolve_clean : 1, w.epoch, w.helpers, w.hand_run, w.inject, w.block_min,
                      (w.side || w.inres) ? w.batch_cnt : nullptr, w.batch_rq, cam, W, out,
                      w.patch, zcount, w.batch_state, w.inres);
   if (w.rstream) {
@@ -2919,8 +2924,8 @@ hipError_t launch_shard_resolve(const LaunchScene& s, int W, int H, int G, int r
                      sc, maxrec, (const DepRec*)w.deprec, w.dep_pix, w.seg_key, w.wcarry,
                      w.seg_start, w.seg_order, w.counters, w.counters + 1, (CinG*)w.cin,
                      w.team_blocks, w.long_len, (TeamState*)w.team, w.trace, w.coop_group,
-                     w.wave_k, w.resolve_k, w.epoch, w.helpers, w.hand_run, w.inject, w.block_min,
-                     nullptr, w.batch_rq, make_cam(s, W, H), W, nullptr, nullptr, nullptr,
+                     w.wave_k, w.resolve_k, w.resolve_clean > 0 ? w.resolve_clean : 1, w.epoch,
+                     w.helpers, w.hand_run, w.inject, w.block_min, nullptr, w.batch_rq, make_cam(s, W, H), W, nullptr, nullptr, nullptr,
                      nullptr, 0);
   if (ev) (void)hipEventRecord(ev[1], stream);
   hipLaunchKernelGGL(k_shard_cin, dim3(row_blocks), dim3(256), 0, stream, rs, o, G, rmax, H,

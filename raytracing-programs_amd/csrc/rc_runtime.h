@@ -79,6 +79,11 @@ struct FrameLog {
   // After the frames' streams are synchronised: every entry must have run (a pending one
   // counts as a failure).  Returns the failures found.
   long long drain();
+  // A failure read back now or earlier and not yet taken (poll() first).
+  bool earlier_failed();
+  // Entry k (a frame's index at its enqueue) has run and its hand-off failed.  Only for an
+  // entry whose stream has been synchronised and that poll() has not read back yet.
+  bool entry_failed(long long k) const;
   // checked / failed since the last take(), then reset.
   void take(long long* c, long long* f);
 };

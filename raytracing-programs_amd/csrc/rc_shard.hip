@@ -83,8 +83,12 @@ struct rc_group {
   // Fixed-size entry exchange (no host synchronisation inside a frame): the DEP entries per
   // rank of the last frame with this key, an upper bound for the next one.  A frame whose
   // count exceeds it is detected at the frame's end and rendered again with exact sizes.
+  // The key is the scene's CONTENT (a hash of its packed image), not its address: every
+  // process of a multi-process group must take the same exchange (ncclGather/ncclScatter of
+  // fixed blocks, or the exact-size ncclSend/ncclRecv), and the bound itself comes from the
+  // frame's all-reduced count, so ranks rendering the same frames reach the same decision.
   struct {
-    const void* scene = nullptr;
+    unsigned long long scene = 0;
     int W = 0, H = 0, maxrec = 0;
     long long per_rank = -1;
   } bound;
@@ -274,6 +278,14 @@ int sync_all(rc_group& g) {
   return 0;
 }
 
+// FNV-1a of the packed scene image (header included): equal on every rank given equal scenes
+unsigned long long scene_key(const rc_packed_header* h) {
+  const unsigned char* p = (const unsigned char*)h;
+  unsigned long long x = 1469598103934665603ull;
+  for (int i = 0; i < h->bytes; ++i) x = (x ^ p[i]) * 1099511628211ull;
+  return x;
+}
+
 double ms_since(std::chrono::steady_clock::time_point t0) {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
@@ -292,18 +304,21 @@ int render_one_rank(rc_group& g, const rc_scene* s, int W, int H, const rc_optio
     d_image = (uint8_t*)r.image.p;
   }
   DevCtx& c = *r.c;
-  if (c.lone_log.poll() > 0) {   // an earlier lone frame of this workspace failed
+  if (c.lone_log.earlier_failed()) {   // an earlier lone frame of this workspace failed
     c.lone_log.take(nullptr, nullptr);
     return -1;
   }
   // the scene upload and the phase events live on the ctx stream: the rank's stream here
   hipStream_t saved = c.stream;
   c.stream = r.stream;
+  const long long own = c.lone_log.head;   // this frame's ring entry
   const int rc = enqueue_render(c, s, W, H, 0, 1, H, opt, d_image, r.stream, true);
   c.stream = saved;
   if (rc) return -1;
   HIP_TRY(hipStreamSynchronize(r.stream));
-  if (c.lone_log.poll() > 0) {
+  const bool failed = c.lone_log.entry_failed(own);
+  c.lone_log.poll();
+  if (failed) {
     c.lone_log.take(nullptr, nullptr);
     return -1;
   }
@@ -341,7 +356,8 @@ int render_sharded(rc_group& g, const rc_scene* s, int W, int H, const rc_option
   const size_t row_bytes = (size_t)W * 3;
   const size_t block_bytes = (size_t)rmax * row_bytes;
   Rank* root = g.root;
-  if (G == 1 && root) return render_one_rank(g, s, W, H, opt, d_image, timing, t0);
+  if (G == 1 && root && tune().shard_lone)
+    return render_one_rank(g, s, W, H, opt, d_image, timing, t0);
   if (root) {
     HIP_TRY(hipSetDevice(root->device));
     if (!d_image) {
@@ -384,9 +400,12 @@ int render_sharded(rc_group& g, const rc_scene* s, int W, int H, const rc_option
                            r.stream));
   }
   if (root) HIP_TRY(hipEventRecord(root->ev[1], root->stream));
-  // fixed-size exchange when the last frame with this key bounds the entry counts
-  const bool fixed = parity && g.bound.per_rank >= 0 && g.bound.scene == s->img &&
+  // fixed-size exchange when the last frame with this key bounds the entry counts; a bound
+  // beyond a rank's pixel count (rc_group_debug_bound) is that count (the buffers' size)
+  const unsigned long long key = parity ? scene_key(s->img) : 0;
+  const bool fixed = parity && g.bound.per_rank >= 0 && g.bound.scene == key &&
                      g.bound.W == W && g.bound.H == H && g.bound.maxrec == maxrec;
+  const long long per_rank = std::min<long long>(g.bound.per_rank, (long long)rmax * W);
   std::vector<size_t> cnt(G, 0);
   if (parity) {
     // 2. row summaries and entry counts to the root
@@ -401,7 +420,7 @@ int render_sharded(rc_group& g, const rc_scene* s, int W, int H, const rc_option
       return -1;
     std::vector<size_t> off(G, 0), eb(G), eo(G), cb(G), co(G);
     if (fixed) {   // every rank's list padded to the bound: sizes known without the counts
-      for (int q = 0; q < G; ++q) cnt[q] = (size_t)g.bound.per_rank;
+      for (int q = 0; q < G; ++q) cnt[q] = (size_t)per_rank;
     } else {   // the counts first (host synchronisation), then the exact sizes
       for (auto& rp : g.ranks) {
         HIP_TRY(hipSetDevice(rp->device));
@@ -459,7 +478,7 @@ int render_sharded(rc_group& g, const rc_scene* s, int W, int H, const rc_option
       hipEvent_t rev[2] = {root->ev[2], root->ev[3]};
       HIP_TRY(rc::launch_shard_resolve(ls[0], W, H, G, rmax, root->rows_all.p, root->ent_all.p,
                                        offs.data(), maxrec, wr, root->cin_ret.p, root->stream,
-                                       rev, fixed ? (int)g.bound.per_rank : 0x7fffffff));
+                                       rev, fixed ? (int)per_rank : 0x7fffffff));
     }
     std::vector<void*> rcv;
     for (size_t i = 0; i < g.ranks.size(); ++i) rcv.push_back(w[i].cin);
@@ -473,7 +492,7 @@ int render_sharded(rc_group& g, const rc_scene* s, int W, int H, const rc_option
       HIP_TRY(hipSetDevice(r.device));
       HIP_TRY(rc::launch_shard_phase_c(ls[i], W, H, r.rank, G, maxrec, (uint8_t*)r.frame.p, w[i],
                                        g.epoch, (unsigned long long*)r.fb.zcount.p, r.stream,
-                                       fixed ? (int)g.bound.per_rank : 0x7fffffff));
+                                       fixed ? (int)per_rank : 0x7fffffff));
     }
   }
   if (root) HIP_TRY(hipEventRecord(root->ev[4], root->stream));
@@ -528,11 +547,11 @@ int render_sharded(rc_group& g, const rc_scene* s, int W, int H, const rc_option
                                                       : (long long)rp->h_small[0];
       if (n > mx) mx = n;
     }
-    if (fixed && mx > g.bound.per_rank) {   // an entry list overflowed the padded exchange
+    if (fixed && mx > per_rank) {   // an entry list overflowed the padded exchange
       g.bound.per_rank = -1;
       return 1;   // render_sharded_retry renders the frame again with exact sizes
     }
-    g.bound.scene = s->img;
+    g.bound.scene = key;
     g.bound.W = W;
     g.bound.H = H;
     g.bound.maxrec = maxrec;
@@ -713,6 +732,8 @@ int rc_render_sharded(rc_group* g, const rc_scene* s, int W, int H, const rc_opt
   return rc;
 }
 
+// Applies to the ranks this process drives: in a multi-process group every rank must make the
+// same call before the same frame (the bound selects the exchange's collectives).
 int rc_group_debug_bound(rc_group* g, long long per_rank) {
   if (!g || per_rank < -1) return -1;
   g->bound.per_rank = per_rank;

@@ -133,6 +133,37 @@ def test_sharded_rccl_one_rank(mode, scenes, table):
         gr.close()
 
 
+@pytest.mark.parametrize("mode", ["parity", "fast"])
+def test_sharded_rccl_one_rank_exchange(mode, scenes, table):
+    """One-rank RCCL groups through the sharded exchange instead of the lone-frame bypass
+    (rc_tuning.shard_lone = 0), on both group kinds: the row-block ncclGather, and in parity the
+    exact-size exchange of a new key (ncclSend/ncclRecv), the fixed-size one of repeated frames
+    (ncclGather / ncclScatter of padded blocks), the ncclAllReduce of the entry counts that
+    bounds the next frame, and an overflowed bound (rendered again exactly).  Every image
+    md5-equal to the reference."""
+    key = "quadric:1024x1024:d6:" + mode
+    want = table[key]["md5"]
+    with rc.tuned(shard_lone=0):
+        gr = rc.Group.rank(1, 0, rc.Group.unique_id(), 0)
+        try:
+            for g in (group([0], "rccl"), gr):
+                for i in range(3):   # exact (new key), then fixed twice
+                    assert p3_md5(sharded(g, scenes["quadric"], 1024, 1024, 6, mode)) == want, i
+                st = g.stats()
+                assert st["ranks"] == 1
+                if mode == "parity":
+                    assert st["dep_pixels"] == table[key].get("dep_pixels", st["dep_pixels"])
+                    assert st["resolve_ms"] > 0.0
+                    g.debug_bound(16)   # the next frame's lists overflow the padded blocks
+                    assert p3_md5(sharded(g, scenes["quadric"], 1024, 1024, 6, mode)) == want
+                    assert p3_md5(sharded(g, scenes["quadric"], 1024, 1024, 6, mode)) == want
+                    g.debug_bound(1 << 40)   # far above any count: clamped to the rank's pixels
+                    assert p3_md5(sharded(g, scenes["quadric"], 1024, 1024, 6, mode)) == want
+                    g.debug_bound(-1)
+        finally:
+            gr.close()
+
+
 def test_sharded_repeat_and_stats(scenes, table):
     """Back-to-back sharded frames reuse every buffer (carry-in tags advance per frame); the
     exchange volumes follow the wire formats (64 B per DEP entry in, 24 B carry-in back)."""
