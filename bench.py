@@ -323,6 +323,25 @@ def make_group(pkg, dist, world, rank, local):
     return pkg.Group.rank(world, rank, bytes(uid.cpu().tolist()), local)
 
 
+def resolver_diag(d):
+    """The bench line's resolver record (rc_resolver_stats_get), outside the timed region: a
+    slow frame's mechanism shows here — per-frame resolver span spread, the resolver's placement
+    against what a CU can hold (a register or LDS overrun halves the workgroups per CU), the
+    team's rounds, and the longest bounded wait per hand-off site."""
+    r = lambda v: round(v, 4)
+    return {"frames": d["frames"],
+            "resolve_ms": {"min": r(d["resolve_ms_min"]), "max": r(d["resolve_ms_max"]),
+                           "mean": r(d["resolve_ms_mean"])} if d["resolve_ms_mean"] else None,
+            "placement": {"workgroups": d["grid"], "cus": d["res_cus"],
+                          "workgroups_per_cu": d["wg_per_cu"],
+                          "workgroups_per_cu_max": d["wg_per_cu_max"],
+                          "regs_per_lane": d["regs"], "scratch_bytes": d["scratch_bytes"],
+                          "lds_bytes": d["lds_bytes"], "team_blocks": d["team_blocks"]},
+            "team_rounds_max": {"scan": d["scan_rounds_max"], "coop_scan": d["cscan_rounds_max"],
+                                "resolve": d["resolve_rounds_max"]},
+            "spin_wait_us_max": d["spin_wait_us_max"]}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -446,12 +465,14 @@ def main():
         single_ms = (time.perf_counter() - ts) * 1e3 / 5
         single_phases = pkg.profile_end()
         lone = pkg.lone_frames_check()   # every lone frame's hand-off words (7 frames)
+        lone_diag = pkg.resolver_stats(lone=True)
         md5 = pkg.p3_md5(out.cpu().numpy())
         single = {"ms": round(single_ms, 4), "value": round(W * H / (single_ms * 1e-3), 1),
                   "note": "one frame at a time (rc_render_device); phases_ms are its phases",
                   "verified": f"{lone['checked'] - lone['failed']}/7 hand-offs, last image md5 "
                               + ("== reference" if md5 == want_md5 else
-                                 "(no golden)" if want_md5 is None else "MISMATCH")}
+                                 "(no golden)" if want_md5 is None else "MISMATCH"),
+                  "resolver_diag": resolver_diag(lone_diag)}
         # phase C after the resolver on the whole device (side=0): the pixel kernels' own
         # time, for roofline_render (a lone frame's k_side runs beside the resolver and waits
         # for its carry-ins, so its span is not compute time)
@@ -497,11 +518,14 @@ def main():
     # hand-offs: every parity frame's latched carry hand-off words (rc_frames_wait /
     # rc_lone_frames_check); bytes: every frame's image against frame 0's on the device, and
     # frame 0's P3 md5 against the reference's golden
+    diag = None   # the timed frames' own resolver record (rc_resolver_stats_get)
     if piped:
         hand = {"checked": int(pipe_tim.get("frames_checked", 0)),
                 "failed": int(pipe_tim.get("frames_failed", 0))}
+        diag = pkg.resolver_stats(lone=False)
     elif parity and not sharded:
         hand = pkg.lone_frames_check()
+        diag = pkg.resolver_stats(lone=True)
     else:
         hand = None   # no carry hand-off in this mode (sharded: checked inside each call)
     if sharded:
@@ -642,6 +666,8 @@ def main():
                                  if spmc and spmc.get("write_bytes") and store_ms else None),
                              "pmc_source": spmc_src},
         }
+        if diag:
+            line["resolver_diag"] = resolver_diag(diag)
         if single:
             line["single_frame"] = single
         if group_err:
@@ -670,16 +696,26 @@ def main():
         dist.barrier()
         ms = (time.perf_counter() - ts) * 1e3 / reps
         st = group.stats()
+        # every rank's own timeline of the last frame (rc_group_rank_stats), gathered over
+        # torch.distributed outside the timed frames: where a rank's time goes
+        mine = group.rank_stats(rank)
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, mine)
         leg = {"value": round(W * H / (ms * 1e-3), 1), "unit": "rays/s", "ms": round(ms, 4),
                "note": (f"one {W}x{H} image row-sharded over {world} GPUs (rc_render_sharded: "
-                        "phase A on every rank, DEP entries gathered to rank 0 over RCCL, "
-                        "serial carry resolver there, carry-ins back, phase C on every rank, "
-                        "row blocks gathered); strong scaling, capped by the resolver")
+                        "phase A on every rank, DEP entries and row blocks gathered to rank 0 "
+                        "over RCCL, serial carry resolver there with phase C inside it); strong "
+                        "scaling, capped by the resolver")
                        if world > 1 else
                        (f"one {W}x{H} image through rc_render_sharded with one rank: nothing "
-                        "to exchange, the rank renders it as a lone frame"),
+                        "to exchange, the rank renders it as a lone frame" if pkg.get_tuning()[
+                            "shard_lone"] else
+                        f"one {W}x{H} image through rc_render_sharded's exchange with one rank "
+                        "(rc_tuning.shard_lone = 0: wire records, gathers, the root's resolver)"),
                "stats": {k: (round(v, 4) if isinstance(v, float) else v)
-                         for k, v in (st or {}).items()}}
+                         for k, v in (st or {}).items()},
+               "per_rank": [{k: (round(v, 4) if isinstance(v, float) else v)
+                             for k, v in q.items()} if q else None for q in per_rank]}
         if rank == 0:
             m = pkg.p3_md5(out.cpu().numpy())
             leg["md5_vs_reference"] = ("equal" if m == want_md5 else "no golden"

@@ -213,6 +213,27 @@ int rc_debug_inject_error(int nth_frame);
  * rc_frames_wait would. */
 int rc_pipe_reset(void);
 
+/* Resolver diagnostics of the current device (a slow frame's own record): lone = 1 covers the
+ * one-frame-at-a-time renders read back since the previous call with lone = 1 (reset), lone =
+ * 0 the last rc_frames_wait window.  resolve_ms_* per frame from the resolver's HIP events (frames
+ * in flight; 0 for lone frames); grid / res_cus = the last frame's resolver workgroups and the CUs
+ * its stream may use; wg_per_cu = workgroups per CU of that placement, wg_per_cu_max = what one
+ * CU can hold with k_resolve's registers and LDS reservation (occupancy API): fewer than the
+ * placement needs would leave the grid partly queued behind resident workgroups; team rounds
+ * = the most rounds of each kind one frame's team made; spin_wait_us_max[site] = the longest
+ * bounded wait of any frame (sites: team hand-off, phase C carry-in, ready queue, helper
+ * queue; waits under 10 us are not recorded). */
+typedef struct rc_resolver_stats {
+  int64_t frames;
+  double resolve_ms_min, resolve_ms_max, resolve_ms_mean;
+  int32_t grid, res_cus, wg_per_cu, wg_per_cu_max;
+  int32_t regs, scratch_bytes, lds_bytes, team_blocks;
+  int32_t scan_rounds_max, cscan_rounds_max, resolve_rounds_max, pad;
+  double spin_wait_us_max[4];
+} rc_resolver_stats;
+_Static_assert(sizeof(rc_resolver_stats) == 112, "rc_resolver_stats layout (ctypes binding)");
+int rc_resolver_stats_get(int lone, rc_resolver_stats *out);
+
 /* Duration (ms) of the last call's dominant kernel on the current device (the carry
  * resolver in parity mode, the render kernel otherwise), from HIP events on its stream. */
 double rc_last_kernel_ms(void);
@@ -287,6 +308,10 @@ typedef struct rc_tuning {
   int shard_lone;         /* 1: a one-rank group renders its image as a lone frame (default);
                              0: through the sharded exchange (wire records, gathers, the
                              root's resolver) like a multi-rank group — test and measurement */
+  int team_cscan;         /* 1: the team leader hands a RESOLVE round back after resolve_k clean
+                             cooperative steps and the team's next SCAN round is one
+                             cooperative step of every team wave (default); 0: the leader's
+                             LANE passes and LANE-only SCAN rounds                            */
 } rc_tuning;
 void rc_default_tuning(rc_tuning *t);
 int rc_set_tuning(const rc_tuning *t);
@@ -332,17 +357,34 @@ typedef struct rc_shard_stats {   /* the last rc_render_sharded, on the root */
   double total_ms;        /* host wall clock of the call                                   */
   double device_ms;       /* root's stream: first kernel to the de-interleaved image        */
   double local_ms;        /* root's own rows: fast: render; parity: phase A + packing       */
-  double exchange_in_ms;  /* parity: end of the root's phase A to the resolver's start      */
+  double exchange_in_ms;  /* parity: end of the root's phase A to the resolver's start (entry
+                             and row-block gathers, de-interleave, scan-order rebuild)       */
   double resolve_ms;      /* parity: image-wide carry resolver on the root                  */
-  double phase_c_ms;      /* parity: resolver end to the end of the root's phase C          */
-  double image_ms;        /* row-block gather + de-interleave                               */
+  double phase_c_ms;      /* parity: the phase C tail after the root's resolver (phase C runs
+                             inside the resolver on the root)                                */
+  double image_ms;        /* fast: row-block gather + de-interleave; parity: the image's copy
+                             into the caller's buffer (the row blocks are gathered before the
+                             resolver, inside exchange_in_ms)                                */
   int64_t dep_pixels;
   int64_t zero_normalize;
   int64_t entry_bytes;    /* DEP entries moved to the root                                  */
-  int64_t carry_bytes;    /* carry-ins moved back                                           */
+  int64_t carry_bytes;    /* carry-ins moved back (0: phase C runs on the root)              */
   int64_t image_bytes;    /* row blocks moved to the root (padded to ceil(H/G) rows)        */
 } rc_shard_stats;
 int rc_group_last_stats(const rc_group *group, rc_shard_stats *out);
+/* One rank's own timeline of the last rc_render_sharded (every rank, root or not; -1 if this
+ * process does not drive `rank`): local_ms = its rows (fast: render; parity: phase A + wire
+ * records), exchange_ms = from there until its row blocks (and parity entries) have left,
+ * total_ms = the whole frame on its stream. */
+typedef struct rc_rank_stats {
+  int rank;
+  int rows;
+  double local_ms;
+  double exchange_ms;
+  double total_ms;
+  int64_t dep_pixels;     /* parity: the rank's own DEP entries */
+} rc_rank_stats;
+int rc_group_rank_stats(const rc_group *group, int rank, rc_rank_stats *out);
 /* Parity frames exchange the DEP entries in fixed-size per-rank blocks (no host
  * synchronisation inside the frame) once a frame of the same scene and size has given the
  * per-rank count; a frame that exceeds it is rendered again with exact sizes.  Test aid: set

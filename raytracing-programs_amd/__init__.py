@@ -92,13 +92,31 @@ class RcShardStats(ctypes.Structure):
                 ("image_bytes", ctypes.c_int64)]
 
 
+class RcRankStats(ctypes.Structure):
+    _fields_ = [("rank", ctypes.c_int), ("rows", ctypes.c_int), ("local_ms", ctypes.c_double),
+                ("exchange_ms", ctypes.c_double), ("total_ms", ctypes.c_double),
+                ("dep_pixels", ctypes.c_int64)]
+
+
+class RcResolverStats(ctypes.Structure):
+    _fields_ = [("frames", ctypes.c_int64), ("resolve_ms_min", ctypes.c_double),
+                ("resolve_ms_max", ctypes.c_double), ("resolve_ms_mean", ctypes.c_double),
+                ("grid", ctypes.c_int32), ("res_cus", ctypes.c_int32),
+                ("wg_per_cu", ctypes.c_int32), ("wg_per_cu_max", ctypes.c_int32),
+                ("regs", ctypes.c_int32), ("scratch_bytes", ctypes.c_int32),
+                ("lds_bytes", ctypes.c_int32), ("team_blocks", ctypes.c_int32),
+                ("scan_rounds_max", ctypes.c_int32), ("cscan_rounds_max", ctypes.c_int32),
+                ("resolve_rounds_max", ctypes.c_int32), ("pad", ctypes.c_int32),
+                ("spin_wait_us_max", ctypes.c_double * 4)]
+
+
 TUNING_FIELDS = ["side", "split_shade", "resolve_shared", "resolve_lds_kb", "resolve_grid",
                  "team_blocks", "helpers", "hand_run", "long_len", "wave_k", "resolve_k", "coop",
                  "dep_fast", "o0", "phase_c_finish", "single_res_cus", "pipe_res_cus",
                  "pipe_resolvers", "pipe_slots", "pipe_timing", "pipe_slotstreams", "overlap_d2h",
                  "staged_d2h", "prefault", "copy_threads", "side_blocks", "comp_stream",
                  "block_min", "pipe_inres", "x0", "resolve_clean",
-                 "shard_lone"]
+                 "shard_lone", "team_cscan"]
 
 
 class RcTuning(ctypes.Structure):
@@ -115,7 +133,8 @@ HIP_EXPORTS = ["raycast", "rc_default_options", "rc_scene_create", "rc_scene_des
                "rc_group_create_local", "rc_group_destroy", "rc_group_size",
                "rc_group_transport", "rc_render_sharded", "rc_group_last_stats",
                "rc_default_tuning", "rc_set_tuning", "rc_get_tuning", "rc_lone_frames_check",
-               "rc_debug_inject_error", "rc_group_debug_bound"]
+               "rc_debug_inject_error", "rc_group_debug_bound", "rc_resolver_stats_get",
+               "rc_group_rank_stats"]
 FRONT_EXPORTS = ["add_new_sphere", "add_new_plane", "add_new_quadric", "free_shape_list",
                  "free_light_list", "add_new_spot_light", "add_new_point_light", "parse_json",
                  "set_to_black", "ppm_WriteOutP3", "ppm_clamp"]
@@ -227,6 +246,8 @@ def _hip_lib_locked():
     lib.rc_lone_frames_check.argtypes = [ctypes.POINTER(ctypes.c_int64),
                                          ctypes.POINTER(ctypes.c_int64)]
     lib.rc_debug_inject_error.argtypes = [ctypes.c_int]
+    lib.rc_resolver_stats_get.argtypes = [ctypes.c_int, ctypes.POINTER(RcResolverStats)]
+    lib.rc_group_rank_stats.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(RcRankStats)]
     _hip = lib
     return lib
 
@@ -417,6 +438,21 @@ def frames_wait(timing=None):
         timing.update({k: getattr(t, k) for k, _ in RcTiming._fields_})
 
 
+SPIN_SITES = ("team_handoff", "phase_c_carry_in", "ready_queue", "helper_queue")
+
+
+def resolver_stats(lone=False):
+    """Resolver diagnostics (rc_resolver_stats_get): the last rc_frames_wait window (frames in
+    flight), or with lone=True the one-frame-at-a-time renders read back since the last such
+    call.  A dict; spin waits by site in microseconds."""
+    st = RcResolverStats()
+    if hip_lib().rc_resolver_stats_get(1 if lone else 0, ctypes.byref(st)) != 0:
+        raise RuntimeError("rc_resolver_stats_get failed")
+    d = {k: getattr(st, k) for k, _ in RcResolverStats._fields_ if k not in ("pad", "spin_wait_us_max")}
+    d["spin_wait_us_max"] = {n: round(st.spin_wait_us_max[i], 1) for i, n in enumerate(SPIN_SITES)}
+    return d
+
+
 def lone_frames_check():
     """Synchronise the device and read back every one-frame-at-a-time parity frame's hand-off
     words since the previous check (rc_lone_frames_check): {"checked": n, "failed": 0}; raises
@@ -573,6 +609,14 @@ class Group:
         if hip_lib().rc_group_last_stats(self._h, ctypes.byref(st)) != 0:
             raise RuntimeError("rc_group_last_stats failed")
         return {k: getattr(st, k) for k, _ in RcShardStats._fields_}
+
+    def rank_stats(self, rank):
+        """One rank's own timeline of the last render (rc_group_rank_stats), or None when this
+        process does not drive that rank."""
+        st = RcRankStats()
+        if hip_lib().rc_group_rank_stats(self._h, int(rank), ctypes.byref(st)) != 0:
+            return None
+        return {k: getattr(st, k) for k, _ in RcRankStats._fields_}
 
     def debug_bound(self, per_rank):
         """Test aid (rc_group_debug_bound): the fixed-size entry exchange's per-rank bound."""

@@ -67,6 +67,7 @@ rc_tuning default_tuning() {
   t.x0 = 1;
   t.resolve_clean = 1;
   t.shard_lone = 1;
+  t.team_cscan = 1;
   // regular segments of >= 3000 entries on whole workgroups when there are workgroups for all
   // of them (k_seg_order): lone quadric 4096^2 5.19 -> 5.06 ms (its ~100 3856-entry segments
   // 4.4 -> 2.5 ms, under the team segment); 8192^2 and pipeline lanes have more such segments
@@ -127,6 +128,12 @@ long long FrameLog::poll() {
                    "at workgroup %d, detail %d/%d\n",
                    tail, what, code, spin_site(code), e->block, e->info, e->info2);
     }
+    ++diag.frames;
+    diag.scan_max = e->n_scan > diag.scan_max ? e->n_scan : diag.scan_max;
+    diag.cscan_max = e->n_cscan > diag.cscan_max ? e->n_cscan : diag.cscan_max;
+    diag.resolve_max = e->n_resolve > diag.resolve_max ? e->n_resolve : diag.resolve_max;
+    for (int q = 0; q < 4; ++q)
+      if (e->spin_ticks[q] > diag.spin_ticks_max[q]) diag.spin_ticks_max[q] = e->spin_ticks[q];
     e->code = kPending;
     ++tail;
     ++checked;
@@ -163,6 +170,28 @@ void FrameLog::take(long long* c, long long* f) {
   if (c) *c = checked;
   if (f) *f = failed;
   checked = failed = 0;
+}
+
+// rc_resolver_stats: the placement and resources part, and a window's frame diagnostics
+int fill_resolver_stats(DevCtx& c, const FrameLog::Diag& d, int grid, int res_cus, int lds,
+                        int team, rc_resolver_stats* r) {
+  r->grid = grid;
+  r->res_cus = res_cus;
+  r->wg_per_cu = res_cus > 0 ? (grid + res_cus - 1) / res_cus : 0;
+  r->lds_bytes = lds;
+  r->team_blocks = team;
+  int regs = 0, scratch = 0, per_cu = 0;
+  if (rc::resolve_resources(lds > 0 ? lds : 0, &regs, &scratch, &per_cu) == 0) {
+    r->regs = regs;
+    r->scratch_bytes = scratch;
+    r->wg_per_cu_max = per_cu;
+  }
+  r->scan_rounds_max = d.scan_max;
+  r->cscan_rounds_max = d.cscan_max;
+  r->resolve_rounds_max = d.resolve_max;
+  for (int q = 0; q < 4; ++q) r->spin_wait_us_max[q] = d.spin_ticks_max[q] * 0.01;
+  (void)c;
+  return 0;
 }
 
 int ctx_get(int device, DevCtx** out) {
@@ -390,7 +419,7 @@ int rc_set_tuning(const rc_tuning* t) {
       in(t->staged_d2h, 0, 1) && in(t->prefault, 0, 1) && in(t->copy_threads, 1, 32) &&
       in(t->comp_stream, 0, 2) && in(t->side_blocks, 0, 1 << 16) &&
       in(t->block_min, 0, 1 << 30) && in(t->pipe_inres, 0, 2) && in(t->x0, 0, 1) &&
-      in(t->resolve_clean, 1, 64) && in(t->shard_lone, 0, 1) &&
+      in(t->resolve_clean, 1, 64) && in(t->shard_lone, 0, 1) && in(t->team_cscan, 0, 1) &&
       !(t->split_shade && !t->side);
   if (!ok) {
     std::fprintf(stderr, "Error: rc_set_tuning: a field is out of range\n");
@@ -631,6 +660,18 @@ int ensure_parity(DevCtx& c, FrameBufs& b, int W, int H, rc::ParityWork& w, int 
   if (tu.team_blocks >= 0) w.team_blocks = tu.team_blocks;
   if (w.team_blocks > 256) w.team_blocks = 256;
   if (w.team_blocks > w.resolve_blocks / 2) w.team_blocks = w.resolve_blocks / 2;
+  // the placement rc_resolver_stats_get reports
+  if (piped) {
+    c.pipe_grid = w.resolve_blocks;
+    c.pipe_res_cus = res_cus;
+    c.pipe_lds = w.resolve_lds;
+    c.pipe_team = w.team_blocks;
+  } else {
+    c.lone_grid = w.resolve_blocks;
+    c.lone_res_cus = res_cus;
+    c.lone_lds = w.resolve_lds;
+    c.lone_team = w.team_blocks;
+  }
   // helper blocks for handed-off dense runs (k_resolve): 8 of the grid for a lone frame
   // (quadric 4096^2 5.85 -> 5.64 ms); none in a pipeline lane, whose grid is a partition's and
   // whose regular waves need those slots more (frames in flight without helpers: reflection
@@ -646,6 +687,7 @@ int ensure_parity(DevCtx& c, FrameBufs& b, int W, int H, rc::ParityWork& w, int 
   w.wave_k = tu.wave_k;
   w.resolve_k = tu.resolve_k;
   w.resolve_clean = tu.resolve_clean;
+  w.team_cscan = tu.team_cscan;
   w.coop_group = 0;
   if (tu.coop && b.scene_src) {
     const int n = ((const rc_packed_header*)b.scene_src)->n;
@@ -1197,9 +1239,25 @@ int rc_frames_wait(rc_timing* timing) {
       if (report_spin_error(p.fb[k], "frames in flight")) rc = -1;
     }
     const int n = !p.rt_on ? 0 : p.submitted < Pipe::kEv ? (int)p.submitted : Pipe::kEv;
-    double sum = 0.0;
-    for (int e = 0; e < n; ++e) sum += event_ms(p.rt[e][0], p.rt[e][1]);
+    double sum = 0.0, lo = 0.0, hi = 0.0;
+    for (int e = 0; e < n; ++e) {
+      const double ms = event_ms(p.rt[e][0], p.rt[e][1]);
+      sum += ms;
+      lo = (e == 0 || ms < lo) ? ms : lo;
+      hi = ms > hi ? ms : hi;
+    }
     if (n > 0) g_last_kernel_ms = sum / n;
+    // the window's resolver record (rc_resolver_stats_get(0, ..))
+    {
+      const FrameLog::Diag d = p.log.diag_take();
+      rc_resolver_stats& r = c->pipe_stats;
+      std::memset(&r, 0, sizeof r);
+      r.frames = d.frames;
+      r.resolve_ms_min = lo;
+      r.resolve_ms_max = hi;
+      r.resolve_ms_mean = n > 0 ? sum / n : 0.0;
+      fill_resolver_stats(*c, d, c->pipe_grid, c->pipe_res_cus, c->pipe_lds, c->pipe_team, &r);
+    }
     if (timing && n > 0 && p.last >= 0) {
       timing->resolve_ms = sum / n;
       FrameBufs& b = p.fb[p.last];
@@ -1243,6 +1301,24 @@ int rc_lone_frames_check(int64_t* checked, int64_t* failed) {
   if (checked) *checked = ch;
   if (failed) *failed = f;
   return f ? -1 : 0;
+}
+
+int rc_resolver_stats_get(int lone, rc_resolver_stats* out) {
+  if (!out) return -1;
+  int dev = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  DevCtx* c;
+  if (ctx_get(dev, &c)) return -1;
+  std::lock_guard<std::mutex> lk(c->mu);
+  if (!lone) {
+    *out = c->pipe_stats;
+    return 0;
+  }
+  c->lone_log.poll();   // the frames whose words have arrived
+  std::memset(out, 0, sizeof *out);
+  const FrameLog::Diag d = c->lone_log.diag_take();
+  out->frames = d.frames;
+  return fill_resolver_stats(*c, d, c->lone_grid, c->lone_res_cus, c->lone_lds, c->lone_team, out);
 }
 
 int rc_debug_inject_error(int nth_frame) {

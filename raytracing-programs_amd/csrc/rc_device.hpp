@@ -577,6 +577,9 @@ __device__ __forceinline__ bool shadow_quadric(V3 O, V3 D, const rc_shape& q, in
 // C/raycast.c:441-531 (shadow_test = true): is any shape hit with 0 < t < inf?  The first
 // such shape is always accepted, so the loop may stop there.
 __device__ __forceinline__ bool shadowed(const Scene& sc, V3 O, V3 D, int skip) {
+#if RC_EXP_NOSHADOW   // timing attribution builds only (wrong images): no shadow rays
+  return false;
+#endif
   const RayK rk = ray_consts(D);
   const bool x0 = quad_x0(sc), rej = x0 && x0_reject(O, D);
   for (int k = 0; k < sc.n; ++k) {
@@ -628,6 +631,9 @@ __device__ __forceinline__ void hit_frame(const Scene& sc, int idx, V3 O, V3 D, 
 
 // calc_color (C/raycast.c:381-421) for shape `idx` (sc.n = the phantom shapes_list[-1]).
 __device__ __forceinline__ V3 shade(const Scene& sc, int idx, V3 P, V3 N, V3 D, int& zero_events) {
+#if RC_EXP_NOSHADE   // timing attribution builds only (wrong images): no shading at all
+  return v3(0.0f, 0.0f, 0.0f);
+#endif
   const rc_shape& o = sc.lshapes[idx];
   const float opacity = o.opacity;
   V3 out = v3(0.0f, 0.0f, 0.0f);
@@ -1244,7 +1250,7 @@ __device__ __forceinline__ V3 carry_path_spec(const Scene& sc, const LaneShape& 
     }
 #endif
     V3 P, Nw;
-    hit_frame_sel<kQuad>(sc.shapes[hit ? w : 0], C, Dw, tw, P, Nw);
+    hit_frame_sel<kQuad>(sc.lshapes[hit ? w : 0], C, Dw, tw, P, Nw);   // divergent: LDS copy
     C = sel(hit, P, C);
     N = sel(hit, Nw, N);
     obj = hit ? w : obj;

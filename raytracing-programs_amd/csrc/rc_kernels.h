@@ -59,6 +59,7 @@ struct ParityWork {
   int wave_k;               // clean cooperative steps before a wave window goes back to LANE
   int resolve_k;            // the same for the team leader's block window
   int resolve_clean;        // clean windows in a row that end a RESOLVE round
+  int team_cscan;           // cooperative SCAN rounds after RESOLVE rounds (early hand-back)
   int coop_group;           // lanes per entry of the cooperative evaluator (0: off)
   unsigned* trace;          // optional [2*nseg] per-segment {ticks, evals} (debug)
   // Pipelined frames (rc_frame_submit): the resolver runs on its own stream (a CU partition
@@ -108,20 +109,17 @@ hipError_t launch_shard_local(const LaunchScene& s, int W, int H, int row0, int 
                               void* ent, void* rows, unsigned long long* zcount,
                               hipStream_t stream);
 // The root: image scan order from the gathered rows ([G][rmax]) and entries (rank g's at
-// offs[g]), the carry resolver, and the carry-ins in the gathered layout (cin_ret).
-// ev (optional): [0] resolver start, [1] resolver end.  bound: entries delivered per rank
-// (the fixed-size exchange; beyond it a rank's list is not read as records).
+// offs[g]) in a lone frame's layout (pixel-indexed records, primary shades and writer carries
+// in w.deprec / w.wcarry, which hold W*H + 1 pixels: the last is a spare for entries beyond a
+// fixed-size exchange's bound), the carry resolver with phase C inside it (w.inres) and the
+// phase C tail, shading every DEP entry into `out` (W*H + 1 pixels; its non-DEP pixels are the
+// gathered row blocks).  ev (optional): [0] resolver start, [1] resolver end.  bound: entries
+// delivered per rank (the fixed-size exchange; beyond it a rank's list is not read as records).
 hipError_t launch_shard_resolve(const LaunchScene& s, int W, int H, int G, int rmax,
                                 const void* rows_all, const void* ent_all,
                                 const long long* offs, int maxrec, const ParityWork& w,
-                                void* cin_ret, hipStream_t stream, const hipEvent_t* ev,
-                                int bound = 0x7fffffff);
-// A rank: phase C of its DEP list once its carry-ins (tag) are in w.cin.
-// limit: carry-ins exist for the first `limit` entries only (fixed-size exchange)
-hipError_t launch_shard_phase_c(const LaunchScene& s, int W, int H, int row0, int row_step,
-                                int maxrec, uint8_t* out, const ParityWork& w, unsigned tag,
-                                unsigned long long* zcount, hipStream_t stream,
-                                int limit = 0x7fffffff);
+                                uint8_t* out, unsigned long long* zcount, hipStream_t stream,
+                                const hipEvent_t* ev, int bound = 0x7fffffff);
 // The root: image <- gathered row blocks [G][rmax][W*3].
 hipError_t launch_deinterleave(const uint8_t* gathered, int G, int rmax, int W, int H,
                                uint8_t* img, hipStream_t stream);
@@ -131,6 +129,9 @@ size_t row_stats_bytes();
 size_t team_state_bytes();
 size_t team_dq_offset();   // DenseQueue {prod, claim, finished} inside TeamState
 int resolve_blocks_resident(int cus, int lds_bytes);
+// k_resolve<true>'s resources: registers per lane (VGPRs + AGPRs), scratch bytes per lane, and
+// the workgroups one CU can hold with `lds_bytes` of dynamic LDS each (occupancy API).
+int resolve_resources(int lds_bytes, int* regs, int* scratch, int* wg_per_cu);
 int side_lds_bytes(int resolve_dyn_lds);
 int phase_c_side_blocks(int cus, int side_lds);
 

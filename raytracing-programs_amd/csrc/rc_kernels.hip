@@ -609,6 +609,15 @@ __global__ void __launch_bounds__(256) k_row_compact(
 // team_blocks*256-entry window per round and agree on the first changer through a counter
 // barrier (all team blocks are co-resident: they are the first blocks of a grid sized to the
 // device's resident capacity).
+#ifndef RC_DIAG
+#define RC_DIAG 0   // 1: the diagnostic builds (make stamps / stamps2) write the resolver trace
+#endif
+#ifndef RC_TEAM_CSCAN
+#define RC_TEAM_CSCAN 1   // 0 compiles the cooperative SCAN rounds out (rc_tuning.team_cscan)
+#endif
+#ifndef RC_RES_GLOBAL_SCAN
+#define RC_RES_GLOBAL_SCAN 0   // measured: global (scalar) records in the LANE loops: lone resolver 4.15 -> 4.35 ms
+#endif
 constexpr int kResolveBlock = 256;
 constexpr int kTeamMax = 256;
 constexpr int kLdsShapes = kLdsShapesMax;
@@ -1088,11 +1097,16 @@ struct BlockWinShared {
 // hp (helper blocks): carry predictor; the cooperative step then takes entry pos at c in
 // group 0 and entry pos+1 at Eb-1 guessed carry-ins in the other groups (wave_window's
 // predictive step with the whole block: 15 guesses instead of 3).
-__device__ __forceinline__ void block_window(const Scene& sc, int maxrec, BlockWinShared& bw,
-                                             int base, int nvalid, V3& c, const LaneShape& ls,
-                                             int G, bool& dense, bool& changed, int K,
-                                             CinG* __restrict__ cin, unsigned tag,
-                                             WinStats& ws, CarryHist* hp = nullptr) {
+// stop (the team leader): instead of a LANE pass after K clean cooperative steps, return at
+// once with the number of entries resolved so far (the team's cooperative SCAN takes the
+// rest, k_resolve).  Returns -1 when the window was resolved to its end.
+__device__ __forceinline__ int block_window(const Scene& sc, int maxrec, BlockWinShared& bw,
+                                            int base, int nvalid, V3& c, const LaneShape& ls,
+                                            int G, bool& dense, bool& changed, int K,
+                                            CinG* __restrict__ cin, unsigned tag,
+                                            WinStats& ws, CarryHist* hp = nullptr,
+                                            bool stop = false) {
+  int stopped = -1;
   constexpr int kNo = 0x7fffffff;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   changed = false;
@@ -1302,13 +1316,20 @@ __device__ __forceinline__ void block_window(const Scene& sc, int maxrec, BlockW
       coop = G > 0;
       clean_run = 0;
     } else if (coop) {
-      if (++clean_run >= K) coop = false;
+      if (++clean_run >= K) {
+        coop = false;
+        if (stop) {   // the cluster is over: the team scans on from pos
+          stopped = pos;
+          break;
+        }
+      }
     }
   }
 #if RC_STAMPS
   if (top_) ws.cs += __builtin_amdgcn_s_memtime() - top_;
 #endif
   dense = coop;
+  return stopped;
 }
 
 // Team hand-off by data-tagged 8-byte granules (MI355X_MICROARCH.md: granule hand-off, R2):
@@ -1352,13 +1373,24 @@ struct TeamState {
   // by k_side's waves in that order (ready_range, phase_c_ready)
   int rq_prod, rq_cons;
   int helpers_out;   // helper workgroups past their hand-off loop (resolver_phase_c, mode 2)
-  int pad[25];
+  // Frame diagnostics, latched with the error word after the frame (FrameLog::Entry): the
+  // team's SCAN (LANE), cooperative SCAN and RESOLVE rounds, and per spin site (kSpin*) the
+  // longest bounded wait of the frame in 10 ns ticks (waits under 10 us are not noted)
+  int n_scan, n_cscan, n_resolve;
+  int spin_ticks[4];
+  int pad[18];
   TeamSlot slot[2][kTeamMax];
   DenseQueue dq;
 };
 
 static_assert(sizeof(TeamState) % 16 == 0, "k_row_stats clears TeamState in 16-byte words");
+// the host's per-frame record (rc_runtime.h FrameLog::Entry) is TeamState's first 64 bytes
+static_assert(offsetof(TeamState, n_scan) == 28 && offsetof(TeamState, spin_ticks) == 40 &&
+                  offsetof(TeamState, pad) == 56,
+              "FrameLog::Entry layout");
 
+// spin sites (TeamState::spin_ticks)
+constexpr int kSpinTeam = 0, kSpinCarry = 1, kSpinQueue = 2, kSpinHelper = 3;
 constexpr unsigned long long kSpinLimit = 500000000ull;   // 5 s of the 100 MHz clock
 constexpr unsigned long long kSpinPoll = 100000ull;       // check the error word after 1 ms
 
@@ -1370,6 +1402,14 @@ __device__ __forceinline__ void set_error(TeamState* ts, int code, int info, int
     __hip_atomic_store(&ts->err_info, info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(&ts->err_info2, info2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+}
+// A bounded spin of `site` that started at t0 is over: note its wait when it was long (a
+// frame's record of what it waited on; one atomic per long wait only).
+__device__ __forceinline__ void spin_note(TeamState* ts, int site, unsigned long long t0) {
+  const unsigned long long dt = __builtin_amdgcn_s_memrealtime() - t0;
+  if (dt > 1000)
+    __hip_atomic_fetch_max(&ts->spin_ticks[site], (int)(dt < 0x7fffffffull ? dt : 0x7fffffffull),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 // A spin that started at t0 gives up: its own limit passed, or (after 1 ms) another spin
 // already failed.
@@ -1443,6 +1483,7 @@ __device__ __forceinline__ bool team_collect(TeamState* ts, int round, int b, un
     const unsigned long long g3 = __hip_atomic_load(&sl->g[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if ((unsigned)(g0 >> 32) == tag && (unsigned)(g1 >> 32) == tag &&
         (unsigned)(g2 >> 32) == tag && (unsigned)(g3 >> 32) == tag) {
+      spin_note(ts, kSpinTeam, t0);
       pos = (unsigned)g0;
       c = v3(__uint_as_float((unsigned)g1), __uint_as_float((unsigned)g2),
              __uint_as_float((unsigned)g3));
@@ -1489,9 +1530,13 @@ __device__ __forceinline__ bool batch_carries(CinG* cin, int ndep, int b, unsign
   bool ok = j >= ndep;
   unsigned long long t0 = 0;
   int seen = -1;
+  const unsigned long long w0 = __builtin_amdgcn_s_memrealtime();
   for (int poll = 0;; ++poll) {
     if (!ok) ok = cin_get(cin, j, tag, c, hit);
-    if (__all(ok)) return true;
+    if (__all(ok)) {
+      if (poll > 0 && (threadIdx.x & 63) == 0) spin_note(ts, kSpinCarry, w0);
+      return true;
+    }
     if (!wait) return false;
     const int progress =
         __popcll(__ballot(ok)) +
@@ -1649,11 +1694,13 @@ __device__ __forceinline__ void phase_c_ready(const Scene& sc, const Cam& cam, i
     int b = -1;
     if ((threadIdx.x & 63) == 0) {
       unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+      const unsigned long long w0 = t0;
       int seen = -1;
       for (;;) {
         const int v = __hip_atomic_load(&rq[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (v) {
           b = v - 1;
+          spin_note(ts, kSpinQueue, w0);
           break;
         }
         const int prod = __hip_atomic_load(&ts->rq_prod, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1713,11 +1760,14 @@ __global__ void __launch_bounds__(kResolveBlock) __attribute__((amdgpu_waves_per
     const int* __restrict__ seg_start, const int* __restrict__ seg_order,
     int* __restrict__ counters, int* __restrict__ head,
     CinG* __restrict__ cin, int team_blocks, int long_len, TeamState* __restrict__ ts,
-    unsigned* __restrict__ trace, int G, int wave_k, int resolve_k, int resolve_clean, unsigned tag,
+    unsigned* __restrict__ trace, int G, int wave_k, int resolve_k, int resolve_clean,
+    int team_cscan, unsigned tag,
     int helpers, int hand_run, int inject, int block_min, int* __restrict__ rq_cnt,
     int* __restrict__ rq, Cam cam, int W, uint8_t* __restrict__ out, uint32_t* __restrict__ patch,
     unsigned long long* __restrict__ zcount, int* __restrict__ batch_state, int inres) {
   if (!RC_X0_RESOLVE) sc.has_quadric = sc.has_quadric != 0;   // no cross-term-free form here (RC_X0_*)
+  // the product build has no trace: its timestamps and counters then hold no registers
+  if (!RC_DIAG) trace = nullptr;
   // census for phase C's side kernel: it only proceeds once every resolver block is resident
   if (threadIdx.x == 0)
     __hip_atomic_fetch_add(&counters[5], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1737,7 +1787,10 @@ __global__ void __launch_bounds__(kResolveBlock) __attribute__((amdgpu_waves_per
     for (int i = threadIdx.x; i < words; i += blockDim.x)
       ((unsigned*)s_shapes)[i] = ((const unsigned*)sc.shapes)[i];
     __syncthreads();
-    sc.shapes = s_shapes;
+    // the divergent reads (the winner's record) go to the LDS copy; the wave-uniform shape
+    // loops of the LANE evaluator keep the global records, which the compiler reads with
+    // scalar loads into SGPRs (an LDS copy there costs a vector LDS round trip per field)
+    if (!RC_RES_GLOBAL_SCAN) sc.shapes = s_shapes;
     sc.lshapes = s_shapes;
   }
 #if RC_STAMPS
@@ -1767,9 +1820,14 @@ __global__ void __launch_bounds__(kResolveBlock) __attribute__((amdgpu_waves_per
     __shared__ int s_pos[4];
     __shared__ float s_o[4][3];
     __shared__ int s_gpos;
+    __shared__ int s_cflag;
     __shared__ float s_nc[3];
     const int T = team_blocks;
     const int window = T * 4 * 64;
+    // cooperative SCAN rounds (team_cscan): E entries per wave, 2G lanes each
+    const int cGE = (G > 0 && 2 * G <= 64) ? 2 * G : 64;
+    const int cE = 64 / cGE;
+    const bool cscan_on = RC_TEAM_CSCAN && team_cscan && G > 0 && 2 * G <= 64;
     int round = 0;
     // the long segments lead the length-ordered queue (k_seg_order): stop at the first
     // shorter one instead of walking the whole segment table with dependent loads (0.4 ms at
@@ -1790,6 +1848,9 @@ __global__ void __launch_bounds__(kResolveBlock) __attribute__((amdgpu_waves_per
       V3 c = seg_init_carry(seg_key, wcarry, s);
       int j = start;
       bool resolve = false;
+      int n_scan_ = 0, n_cscan_ = 0, n_resolve_ = 0;   // this segment's rounds by kind
+      // the next SCAN round is cooperative (after a RESOLVE round that handed back early)
+      bool cscan = false;
       // SCAN width: sub-windows of `window` entries per round, doubled after every clean
       // round up to 4 (a clean stretch then costs one hand-off per 4 windows), back to 1 after
       // a changer; the same on every team block (it follows the agreed positions)
@@ -1806,18 +1867,59 @@ __global__ void __launch_bounds__(kResolveBlock) __attribute__((amdgpu_waves_per
         const int j_round = j;
         WinStats tws = {0, 0, 0};
         const bool was_resolve = resolve;
+        const bool coop_scan = RC_TEAM_CSCAN && !resolve && cscan;
+        n_resolve_ += resolve ? 1 : 0;
+        n_cscan_ += coop_scan ? 1 : 0;
+        n_scan_ += (!resolve && !coop_scan) ? 1 : 0;
         if (!resolve) {
           // ---------------------------------------------------------------- SCAN
-          // sub-window q: entries j + q*window + (block*4 + wave)*64 + lane; a wave stops at
-          // its first changer (everything after it in scan order is after it in the window)
+          // LANE: sub-window q: entries j + q*window + (block*4 + wave)*64 + lane; a wave stops
+          // at its first changer (everything after it in scan order is after it in the window).
+          // COOP (right after a RESOLVE round, whose cluster may go on a few entries later):
+          // one cooperative step of every team wave, E entries each at a cooperative
+          // evaluation's latency — T*4*E entries (2 048 at G = 8) in ~1/4 of a LANE round.
           const int slice = ((int)blockIdx.x * 4 + wave) * 64;
           unsigned long long hmq[4] = {0, 0, 0, 0};
+          int wpos = 0x7fffffff;
+          V3 wo = c;
+          const int ci = j + ((int)blockIdx.x * 4 + wave) * cE + lane / cGE;   // COOP: entry
+          bool chit = false;   // COOP: the lane's entry hit some level (its group leader's flag)
+          if (coop_scan) {
+            const bool act = lane / cGE < cE && ci < end;
+            DepRec ri;
+            if (act) ri = rec_at(deprec, dep_pix, ci);
+            V3 oc = c;
+            bool hg = false;
+            int zero = 0;
+#if RC_STAMPS
+            Stamps sts = {{0, 0, 0, 0}, 0};
+#define RC_SPEC1(GT, Q) carry_path_spec<GT, Q>(sc, ls, kself_, G, half_, ri, maxrec, c, zero, hg, &sts)
+#else
+#define RC_SPEC1(GT, Q) carry_path_spec<GT, Q>(sc, ls, kself_, G, half_, ri, maxrec, c, zero, hg)
+#endif
+#define RC_SPEC(GT) \
+  (sc.has_quadric ? (quad_x0(sc) ? RC_SPEC1(GT, 2) : RC_SPEC1(GT, 1)) : RC_SPEC1(GT, 0))
+            const int kself_ = lane % G, half_ = (lane / G) & 1;
+            if (act) {
+              if (G == 8) oc = RC_SPEC(8);
+              else if (G == 4) oc = RC_SPEC(4);
+              else if (G == 16) oc = RC_SPEC(16);
+              else oc = RC_SPEC(0);
+            }
+#undef RC_SPEC
+#undef RC_SPEC1
+            chit = hg;
+            const unsigned long long m = __ballot(act && (lane % cGE) == 0 && !same_bits(oc, c));
+            if (m) {
+              const int gl = __ffsll((long long)m) - 1;
+              wpos = j + ((int)blockIdx.x * 4 + wave) * cE + gl / cGE;
+              wo = v3(__shfl(oc.x, gl, 64), __shfl(oc.y, gl, 64), __shfl(oc.z, gl, 64));
+            }
+          } else {
           // one record ahead (two live, not four: the lanes' two resolver workgroups per CU
           // need the kernel within 256 registers)
           DepRec cur;
           if (j + slice + lane < end) cur = rec_at(deprec, dep_pix, j + slice + lane);
-          int wpos = 0x7fffffff;
-          V3 wo = c;
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             if (q < width && wpos == 0x7fffffff) {
@@ -1841,6 +1943,7 @@ __global__ void __launch_bounds__(kResolveBlock) __attribute__((amdgpu_waves_per
                 wo = v3(__shfl(o.x, k, 64), __shfl(o.y, k, 64), __shfl(o.z, k, 64));
               }
             }
+          }
           }
           if (lane == 0) {
             s_pos[wave] = wpos;
@@ -1887,6 +1990,10 @@ __global__ void __launch_bounds__(kResolveBlock) __attribute__((amdgpu_waves_per
           // entries before the first changer, and the changer itself, read carry c (gpos =
           // 0x7fffffff: every entry of the round); a wave that stopped early has no entry
           // at or before gpos in its later sub-windows
+          if (coop_scan) {
+            if (ci < end && lane / cGE < cE && (lane % cGE) == 0 && ci <= gpos)
+              cin_put(cin, ci, c, tag, chit);
+          } else {
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             if (q < width) {
@@ -1897,9 +2004,16 @@ __global__ void __launch_bounds__(kResolveBlock) __attribute__((amdgpu_waves_per
               if (hi > 0) cin_put_wave_uniform(cin, base, 0, hi, c, tag, hmq[q]);
             }
           }
+          }
           if (gpos == 0x7fffffff) {
-            j += width * window;
-            width = width < 4 ? 2 * width : 4;
+            if (coop_scan) {
+              j += T * 4 * cE;   // no change nearby: LANE rounds from here
+              width = 1;
+            } else {
+              j += width * window;
+              width = width < 4 ? 2 * width : 4;
+            }
+            cscan = false;
           } else {
             j = gpos + 1;
             c = v3(s_nc[0], s_nc[1], s_nc[2]);
@@ -1922,8 +2036,14 @@ __global__ void __launch_bounds__(kResolveBlock) __attribute__((amdgpu_waves_per
               const int jn = j + nv;
               if (jn + t < end) nxt = rec_at(deprec, dep_pix, jn + t);
               bool changed;
-              block_window(sc, maxrec, s_bw, j, nv, c, ls, G, dense, changed, resolve_k, cin,
-                           tag, tws);
+              const int stop = block_window(sc, maxrec, s_bw, j, nv, c, ls, G, dense, changed,
+                                            resolve_k, cin, tag, tws, nullptr, cscan_on);
+              if (stop >= 0) {   // resolve_k clean cooperative steps: the team scans on
+                j += stop;
+                cscan = true;
+                __syncthreads();
+                break;
+              }
               j = jn;
               __syncthreads();   // everyone is done reading this window's records
               // resolve_clean clean windows in a row: the cluster is over (the next one is
@@ -1934,7 +2054,9 @@ __global__ void __launch_bounds__(kResolveBlock) __attribute__((amdgpu_waves_per
               if (j + t < end) s_bw.rec[t] = nxt;
               __syncthreads();
             }
-            if (threadIdx.x == 0) team_publish(ts, round, (unsigned)j, c);
+            // bit 31: the next SCAN round is cooperative (the round ended early)
+            if (threadIdx.x == 0)
+              team_publish(ts, round, (unsigned)j | (cscan ? 0x80000000u : 0u), c);
           }
           if (crediter && T > 1) {
             ready_range(rq_cnt, rq, ts, ndep, pend0, pend1);
@@ -1944,7 +2066,8 @@ __global__ void __launch_bounds__(kResolveBlock) __attribute__((amdgpu_waves_per
             unsigned upos = 0;
             V3 oc;
             const bool ok = team_collect(ts, round, 0, upos, oc);
-            s_gpos = ok ? (int)upos : -1;
+            s_gpos = ok ? (int)(upos & 0x7fffffffu) : -1;
+            s_cflag = (int)(upos >> 31);
             s_nc[0] = oc.x;
             s_nc[1] = oc.y;
             s_nc[2] = oc.z;
@@ -1954,6 +2077,7 @@ __global__ void __launch_bounds__(kResolveBlock) __attribute__((amdgpu_waves_per
           j = s_gpos;
           c = v3(s_nc[0], s_nc[1], s_nc[2]);
           resolve = false;
+          cscan = s_cflag != 0;
           __syncthreads();
         }
         // the round's entries [j_round, j) are published: credited during the next round's
@@ -1965,7 +2089,7 @@ __global__ void __launch_bounds__(kResolveBlock) __attribute__((amdgpu_waves_per
         // debug trace: per-round team log after the per-segment records and stamps
         if (trace && blockIdx.x == 0 && wave == 0 && lane == 0 && round < 8192) {
           unsigned* tl = trace + 3 * (size_t)ndep + 4 * (size_t)nseg + 8 * (size_t)round;
-          tl[0] = was_resolve ? 1u : 0u;
+          tl[0] = was_resolve ? 1u : (coop_scan ? 2u : 0u);
           tl[1] = (unsigned)j_round;
           tl[2] = (unsigned)j;
           tl[3] = (unsigned)(__builtin_amdgcn_s_memtime() - c_round);
@@ -1982,6 +2106,11 @@ __global__ void __launch_bounds__(kResolveBlock) __attribute__((amdgpu_waves_per
         }
       }
       if (crediter) ready_range(rq_cnt, rq, ts, ndep, pend0, pend1);   // the last round's
+      if (blockIdx.x == 0 && threadIdx.x == 0) {   // the frame's record (FrameLog)
+        ts->n_scan += n_scan_;
+        ts->n_cscan += n_cscan_;
+        ts->n_resolve += n_resolve_;
+      }
       if (trace && blockIdx.x == 0 && threadIdx.x == 0) {
         trace[3 * s] = (unsigned)(__builtin_amdgcn_s_memrealtime() - t_seg);
         trace[3 * s + 1] = (unsigned)rounds_here | 0x80000000u;
@@ -2011,10 +2140,12 @@ __global__ void __launch_bounds__(kResolveBlock) __attribute__((amdgpu_waves_per
         // the limit measures a lack of progress: it restarts whenever a regular wave
         // finishes or hands a run off
         unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        const unsigned long long w0 = t0;
         int seen = -1;
         for (;;) {
           if (__hip_atomic_load(&slot.ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == k + 1) {
             got = k;
+            spin_note(ts, kSpinHelper, w0);
             break;
           }
           // Acquire on `finished` (released by each wave after its last possible hand-off)
@@ -2458,25 +2589,27 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_
 // ------------------------------------------------------ row shards (rc_shard.hip) --
 // A parity image split over G ranks by rows (row y -> rank y % G, local row y / G; SURVEY.md
 // §8e).  Every rank runs phase A on its rows into rank-local buffers and packs its DEP entries
-// (k_shard_pack); the root gathers them, rebuilds the image's scan order (k_shard_rows,
-// k_row_scan, k_shard_unpack), resolves the carry chain and sends every rank its entries'
-// carry-ins back (k_shard_cin) for phase C on the rank.  Entries travel in the rank's local
-// scan order, which is the image's scan order restricted to the rank's rows.
+// (k_shard_pack); the root gathers them and the ranks' row blocks (every non-DEP pixel is final
+// after phase A), rebuilds the image's scan order in a lone frame's layout (k_shard_rows,
+// k_row_scan, k_shard_unpack) and runs a lone frame's resolver with phase C inside it, which
+// shades every DEP entry into the root's image.  Entries travel in the rank's local scan order,
+// which is the image's scan order restricted to the rank's rows.
 //
 // A DEP entry on the wire: its record (pad = image pixel, pad2 = the last writer pixel before
-// it in the same row, -1 = none) and that writer's carry-out.  A row's summary: the RowStats
+// it in the same row, -1 = none), that writer's carry-out and the entry's primary shade.  A row's summary: the RowStats
 // fields in image pixel indices, the row's first entry in the rank's list and the carry-out of
 // the row's last writer (the key of a segment that starts after this row).
 struct ShardEntry {
   DepRec rec;
-  float4 kc;
+  float4 kc;     // carry-out of the last writer before the entry in its row
+  float4 pcol;   // the entry's primary shade (phase A, Scene::dep_fast): phase C runs on the root
 };
 struct RowShard {
   int ndep, nstart, loff, pad;
   long long lastw, lastd, wfirst;
   float4 cw;
 };
-static_assert(sizeof(ShardEntry) == 64 && sizeof(RowShard) == 64, "wire records");
+static_assert(sizeof(ShardEntry) == 80 && sizeof(RowShard) == 64, "wire records");
 
 // One wave per local row: the rank's DEP list (local pixels, phase C's index), its wire
 // entries (at the local DEP offsets of k_row_scan) and the row summary.
@@ -2516,6 +2649,7 @@ __global__ void __launch_bounds__(256) k_shard_pack(
       e.rec.pad = (int)(gbase + x);
       e.rec.pad2 = kw >= 0 ? (int)(gbase + kw) : -1;
       e.kc = kw >= 0 ? wcarry[lbase + kw] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      e.pcol = wcarry[lbase + x];   // a DEP pixel's slot: its primary shade (dep_fast)
       ent[l] = e;
     }
     l0 += __popcll(md);
@@ -2550,20 +2684,24 @@ __global__ void __launch_bounds__(256) k_shard_rows(const RowShard* __restrict__
   rs[y] = RowStats{r.ndep, r.nstart, r.lastw, r.lastd, r.wfirst};
 }
 
-// Root, one wave per image row: the row's entries in scan order -> the resolver's inputs.
-// Records are stored densely (entry j at j, dep_pix the identity) and segment keys index a
-// dense carry table (segment s's initial carry at wcarry[s]), so the resolver is unchanged.
-// A segment start is decided exactly as in k_row_compact (writer after the previous DEP).
+// Root, one wave per image row: the row's entries in scan order -> the resolver's inputs, in a
+// lone frame's layout (image pixel indices): the record at deprec[pixel], dep_pix = the
+// pixels in scan order, the entry's primary shade at wcarry[pixel] and every segment's key =
+// the image pixel of the writer before it, whose carry-out goes to wcarry[writer] (a DEP
+// pixel and a writer are never the same pixel).  The resolver, phase C inside it and its
+// framebuffer stores then run exactly as in a lone frame, into the root's image.  A segment
+// start is decided exactly as in k_row_compact (writer after the previous DEP).
 __global__ void __launch_bounds__(256) k_shard_unpack(
     const RowShard* __restrict__ rsall, const ShardEntry* __restrict__ ent, ShardOffs offs,
     int G, int rmax, int W, int H, const int* __restrict__ row_off,
     const int* __restrict__ row_soff, const long long* __restrict__ row_prevw,
     const long long* __restrict__ row_prevd, DepRec* __restrict__ deprec,
     long long* __restrict__ dep_pix, int* __restrict__ seg_start,
-    long long* __restrict__ seg_key, float4* __restrict__ keycarry, int bound) {
+    long long* __restrict__ seg_key, float4* __restrict__ wcarry, int bound) {
   const int y = blockIdx.x * kRowWaves + (int)(threadIdx.x >> 6);
   if (y >= H) return;
   const int lane = threadIdx.x & 63;
+  const long long P = (long long)W * H;
   const int g = y % G;
   const RowShard r = rsall[(size_t)g * rmax + y / G];
   const ShardEntry* e = ent + offs.off[g] + r.loff;
@@ -2585,14 +2723,18 @@ __global__ void __launch_bounds__(256) k_shard_unpack(
     if (valid) q = e[i];
     // bound: the fixed-size exchange delivered each rank's first `bound` entries.  A longer
     // list (the frame is then rendered again, rc_shard.hip) reads the next rank's block: such
-    // an entry becomes a harmless record (zero directions, shape 0) continuing its segment,
-    // never an out-of-range shape index for the resolver
-    if (valid && r.loff + i >= bound) {
+    // an entry becomes a harmless record (zero directions, shape 0) at the spare pixel P (the
+    // root's buffers hold P + 1 pixels), continuing its segment — never an out-of-range shape
+    // or pixel index for the resolver and phase C
+    const bool spare = valid && (r.loff + i >= bound || q.rec.pad < 0 || q.rec.pad >= P);
+    if (spare) {
       q.rec = DepRec{0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0, -1, 0.0f, 0.0f, 0.0f, -1};
       q.kc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      q.pcol = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     }
-    const long long pix = valid ? (q.rec.pad >= 0 ? (long long)q.rec.pad : pd) : -1;
-    const long long kin = valid ? (long long)q.rec.pad2 : -1;
+    const long long pix = valid ? (spare ? P : (long long)q.rec.pad) : -1;
+    const long long kin = valid && !spare && q.rec.pad2 >= 0 && q.rec.pad2 < P
+                              ? (long long)q.rec.pad2 : -1;
     long long prev = __shfl_up(pix, 1, 64);
     if (lane == 0) prev = pd;
     const long long kw = kin >= 0 ? kin : pw;
@@ -2600,36 +2742,21 @@ __global__ void __launch_bounds__(256) k_shard_unpack(
     const unsigned long long ms = __ballot(st);
     if (valid) {
       const int idx = idx0 + i;
-      deprec[idx] = q.rec;
-      dep_pix[idx] = idx;
+      deprec[pix] = q.rec;
+      wcarry[pix] = q.pcol;
+      dep_pix[idx] = pix;
       if (st) {
         const int s = s0 + __popcll(ms & lt);
         seg_start[s] = idx;
-        seg_key[s] = kw >= 0 ? s : -1;
-        keycarry[s] = kin >= 0 ? q.kc : pwc;
+        seg_key[s] = kw;
+        if (kw >= 0) wcarry[kw] = kin >= 0 ? q.kc : pwc;   // every entry keyed by kw writes
+                                                           // the same carry-out
       }
     }
     s0 += __popcll(ms);
     const int last = (n - i0 < 64 ? n - i0 : 64) - 1;
     pd = __shfl(pix, last, 64);
   }
-}
-
-// Root, one wave per image row: the row's resolved carry-ins, back in the owning rank's list
-// order (the gathered entry list's layout).
-__global__ void __launch_bounds__(256) k_shard_cin(const RowShard* __restrict__ rsall,
-                                                   ShardOffs offs, int G, int rmax, int H,
-                                                   const int* __restrict__ row_off,
-                                                   const CinG* __restrict__ cin,
-                                                   CinG* __restrict__ ret) {
-  const int y = blockIdx.x * kRowWaves + (int)(threadIdx.x >> 6);
-  if (y >= H) return;
-  const int lane = threadIdx.x & 63;
-  const int g = y % G;
-  const RowShard r = rsall[(size_t)g * rmax + y / G];
-  CinG* dst = ret + offs.off[g] + r.loff;
-  const CinG* src = cin + row_off[y];
-  for (int i = lane; i < r.ndep; i += 64) dst[i] = src[i];
 }
 
 // Root: image row y <- gathered[y % G][y / G] (the row-cyclic partition undone).
@@ -2749,7 +2876,7 @@ hipError_t launch_parity(const LaunchScene& s, int W, int H, int maxrec, uint8_t
                      maxrec, (const DepRec*)w.deprec, w.dep_pix, w.seg_key, w.wcarry,
                      w.seg_start, w.seg_order, w.counters, w.counters + 1, (CinG*)w.cin, w.team_blocks,
                      w.long_len, (TeamState*)w.team, w.trace, w.coop_group, w.wave_k,
-                     w.resolve_k, w.resolve_clean > 0 ? w.resolve_clean : 1, w.epoch, w.helpers, w.hand_run, w.inject, w.block_min,
+                     w.resolve_k, w.resolve_clean > 0 ? w.resolve_clean : 1, w.team_cscan, w.epoch, w.helpers, w.hand_run, w.inject, w.block_min,
                      (w.side || w.inres) ? w.batch_cnt : nullptr, w.batch_rq, cam, W, out,
                      w.patch, zcount, w.batch_state, w.inres);
   if (w.rstream) {
@@ -2864,6 +2991,19 @@ int resolve_blocks_resident(int cus, int lds_bytes) {
   return per_cu * cus;
 }
 
+int resolve_resources(int lds_bytes, int* regs, int* scratch, int* wg_per_cu) {
+  hipFuncAttributes a{};
+  if (hipFuncGetAttributes(&a, (const void*)k_resolve<true>) != hipSuccess) return -1;
+  if (regs) *regs = a.numRegs;
+  if (scratch) *scratch = (int)a.localSizeBytes;
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_resolve<true>, kResolveBlock,
+                                                   lds_bytes) != hipSuccess)
+    return -1;
+  if (wg_per_cu) *wg_per_cu = per_cu;
+  return 0;
+}
+
 // ----------------------------------------------------------- row-shard launchers --
 size_t shard_entry_bytes() { return sizeof(ShardEntry); }
 size_t shard_row_bytes() { return sizeof(RowShard); }
@@ -2897,10 +3037,11 @@ hipError_t launch_shard_local(const LaunchScene& s, int W, int H, int row0, int 
 hipError_t launch_shard_resolve(const LaunchScene& s, int W, int H, int G, int rmax,
                                 const void* rows_all, const void* ent_all,
                                 const long long* offs, int maxrec, const ParityWork& w,
-                                void* cin_ret, hipStream_t stream, const hipEvent_t* ev,
-                                int bound) {
-  if (G < 1 || G > kMaxShards) return hipErrorInvalidValue;
+                                uint8_t* out, unsigned long long* zcount, hipStream_t stream,
+                                const hipEvent_t* ev, int bound) {
+  if (G < 1 || G > kMaxShards || w.side || w.patch) return hipErrorInvalidValue;
   const Scene sc = make_scene(s);
+  const Cam cam = make_cam(s, W, H);
   ShardOffs o{};
   for (int g = 0; g < G; ++g) o.off[g] = offs[g];
   const RowShard* rs = (const RowShard*)rows_all;
@@ -2919,31 +3060,20 @@ hipError_t launch_shard_resolve(const LaunchScene& s, int W, int H, int G, int r
                      w.seg_order, w.batch_state, w.batch_cnt, w.batch_rq, w.block_min,
                      w.resolve_blocks - w.team_blocks - w.helpers, 1);
   if (ev) (void)hipEventRecord(ev[0], stream);
+  // a lone frame's resolver from here on: phase C inside it (w.inres) shades every DEP entry
+  // of the image into `out` — the root's image, whose non-DEP pixels the gathered row blocks
+  // already hold — and k_finish takes what its waves left
   auto kres = s.n <= kLdsShapes ? k_resolve<true> : k_resolve<false>;
   hipLaunchKernelGGL(kres, dim3(w.resolve_blocks), dim3(kResolveBlock), w.resolve_lds, stream,
                      sc, maxrec, (const DepRec*)w.deprec, w.dep_pix, w.seg_key, w.wcarry,
                      w.seg_start, w.seg_order, w.counters, w.counters + 1, (CinG*)w.cin,
                      w.team_blocks, w.long_len, (TeamState*)w.team, w.trace, w.coop_group,
-                     w.wave_k, w.resolve_k, w.resolve_clean > 0 ? w.resolve_clean : 1, w.epoch,
-                     w.helpers, w.hand_run, w.inject, w.block_min, nullptr, w.batch_rq, make_cam(s, W, H), W, nullptr, nullptr, nullptr,
-                     nullptr, 0);
+                     w.wave_k, w.resolve_k, w.resolve_clean > 0 ? w.resolve_clean : 1,
+                     w.team_cscan, w.epoch, w.helpers, w.hand_run, w.inject, w.block_min,
+                     w.inres ? w.batch_cnt : nullptr, w.batch_rq, cam, W, out, (uint32_t*)nullptr,
+                     zcount, w.batch_state, w.inres);
   if (ev) (void)hipEventRecord(ev[1], stream);
-  hipLaunchKernelGGL(k_shard_cin, dim3(row_blocks), dim3(256), 0, stream, rs, o, G, rmax, H,
-                     w.row_off, (const CinG*)w.cin, (CinG*)cin_ret);
-  return hipGetLastError();
-}
-
-hipError_t launch_shard_phase_c(const LaunchScene& s, int W, int H, int row0, int row_step,
-                                int maxrec, uint8_t* out, const ParityWork& w, unsigned tag,
-                                unsigned long long* zcount, hipStream_t stream, int limit) {
-  const Scene sc = make_scene(s);
-  const Cam cam = make_cam(s, W, H);
-  hipLaunchKernelGGL((s.dep_fast ? (stage_fits(s) ? k_dep_chunks<true, true> : k_dep_chunks<false, true>)
-                                  : (stage_fits(s) ? k_dep_chunks<true, false> : k_dep_chunks<false, false>)),
-                     dim3(w.phase_c_blocks), dim3(kBlock), 0, stream, sc, cam, W, row0, row_step,
-                     maxrec, w.dep_pix, (const DepRec*)w.deprec, (const float4*)w.wcarry,
-                     (CinG*)w.cin, w.counters, out, (uint32_t*)nullptr, zcount,
-                     (TeamState*)w.team, tag, limit);
+  enqueue_phase_c(sc, cam, stage_fits(s), W, H, maxrec, out, w, zcount, stream);
   return hipGetLastError();
 }
 

@@ -64,7 +64,19 @@ struct FrameLog {
   static constexpr int kPending = 0x7fffffff;
   struct Entry {
     int code, block, info, info2;   // TeamState.error, err_block, err_info, err_info2
+    int rq_prod, rq_cons, helpers_out;
+    int n_scan, n_cscan, n_resolve; // the frame's team rounds by kind
+    int spin_ticks[4];              // its longest bounded waits per spin site (10 ns ticks)
+    int pad[2];
   };
+  // Frame diagnostics of the entries read back since the last diag_take(): frames, the most
+  // team rounds of each kind in one frame, the longest wait per spin site.
+  struct Diag {
+    long long frames = 0;
+    int scan_max = 0, cscan_max = 0, resolve_max = 0;
+    int spin_ticks_max[4] = {0, 0, 0, 0};
+  };
+  Diag diag;
   Entry* ring = nullptr;     // pinned host memory, kRing entries
   long long head = 0;        // frames logged
   long long tail = 0;        // frames whose entry has been read back (in order)
@@ -86,6 +98,12 @@ struct FrameLog {
   bool entry_failed(long long k) const;
   // checked / failed since the last take(), then reset.
   void take(long long* c, long long* f);
+  // the diagnostics since the last diag_take(), then reset
+  Diag diag_take() {
+    Diag d = diag;
+    diag = Diag{};
+    return d;
+  }
 };
 
 // Pipelined parity frames (rc_frame_submit).  The device's CUs are split in two partitions
@@ -166,6 +184,11 @@ struct DevCtx {
   size_t pin_bytes = 0;           // capacity of each pinned buffer, in entries
   int* pin_cnt = nullptr;         // pinned: counters[0..3]
   FrameLog lone_log;   // every parity frame rendered in `fb` (rc_render, rc_render_device)
+  // rc_resolver_stats: the last rc_frames_wait window's record (frames in flight), and the
+  // resolver placement of the last frame of each kind (grid, CUs it may use)
+  rc_resolver_stats pipe_stats{};
+  int lone_grid = 0, lone_res_cus = 0, lone_lds = 0, lone_team = 0;
+  int pipe_grid = 0, pipe_res_cus = 0, pipe_lds = 0, pipe_team = 0;
   // `fb` is shared by every one-frame-at-a-time call on this device, and rc_render_device
   // returns before its frame has run: the next enqueue on `fb` from another stream waits for
   // the previous one (ws_ev, recorded after it on ws_stream).
@@ -183,6 +206,8 @@ extern DevCtx g_ctx[kMaxDevices];
 // taken under the tuning lock, so a render reads one consistent set of fields
 rc_tuning tune();
 int ctx_get(int device, DevCtx** out);
+int fill_resolver_stats(DevCtx& c, const FrameLog::Diag& d, int grid, int res_cus, int lds,
+                        int team, rc_resolver_stats* r);
 int copy_to_host(DevCtx& c, uint8_t* host, const uint8_t* dev, size_t bytes, hipStream_t st);
 void prefault(uint8_t* p, size_t n);
 int upload_scene(FrameBufs& b, hipStream_t stream, const rc_scene* s, rc::LaunchScene& ls);

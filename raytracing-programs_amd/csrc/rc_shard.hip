@@ -7,12 +7,12 @@
 // xGMI) and undoes the interleave on the device (k_deinterleave).
 //
 // Parity mode adds the carry chain's exchange (C/raycast.c:340 scan-order carry): every rank
-// runs phase A on its rows and packs its DEP entries (record + in-row writer key and carry) and
-// per-row summaries; the root gathers them (ncclGather of the row summaries, ncclSend/ncclRecv
-// of the variable-length entry lists), rebuilds the image's scan order, runs the carry
-// resolver and returns each rank its entries' carry-ins (ncclSend/ncclRecv); every rank then
-// runs phase C on its rows and the framebuffers are gathered as in fast mode.  The resolver
-// stays serial on the root, so parity scaling is capped by it.
+// runs phase A on its rows and packs its DEP entries (record + in-row writer key and carry +
+// primary shade) and per-row summaries; the root gathers them (ncclGather of the row
+// summaries, ncclGather / ncclSend-ncclRecv of the entry lists) and the row blocks, whose
+// non-DEP pixels are final, rebuilds the image's scan order and runs a lone frame's carry
+// resolver with phase C inside it, which shades every DEP entry into the root's image.  The
+// resolver stays serial on the root, so parity scaling is capped by it.
 //
 // A group is either one rank of a multi-process job (one process per GPU, rc_group_create_rank,
 // the ncclUniqueId shared by the caller) or every rank in this process (rc_group_create_local:
@@ -61,14 +61,17 @@ struct Rank {
   DevBuf frame;                 // local framebuffer, rmax rows
   DevBuf ent, rows;             // wire: DEP entries, row summaries
   DevBuf small;                 // [0] int: DEP entries; [2..3] u64: zero-normalize events
-  int* h_small = nullptr;       // pinned copy of `small`
+  int* h_small = nullptr;       // pinned copy of `small` ([10..11]: the root's phase C events)
   int nrows = 0;
   long long ndep = 0;
+  hipEvent_t rev[4] = {};       // this rank's timeline: start, rows done, sends done, frame end
+  rc_rank_stats last{};
   // root only
   FrameBufs rootfb;             // image-wide resolver workspace
-  DevBuf rows_all, ent_all, cin_ret, frames_all, small_all, image;
+  DevBuf rows_all, ent_all, frames_all, small_all, image;
   int* h_small_all = nullptr;   // pinned, kMaxShards x 4 ints
-  hipEvent_t ev[6] = {};        // root timeline: start, phase A, resolver start/end, phase C, image
+  hipEvent_t ev[6] = {};        // root timeline: start, phase A, resolver start/end, phase C
+                                // tail, image complete
 };
 
 }  // namespace
@@ -103,6 +106,7 @@ int init_rank(Rank& r, int rank, int device) {
   if (ctx_get(device, &r.c)) return -1;
   HIP_TRY(hipStreamCreateWithFlags(&r.stream, hipStreamNonBlocking));
   HIP_TRY(hipEventCreateWithFlags(&r.ready, hipEventDisableTiming));
+  for (auto& e : r.rev) HIP_TRY(hipEventCreate(&e));
   HIP_TRY(hipHostMalloc((void**)&r.h_small, 64, hipHostMallocDefault));
   if (r.small.ensure(64) || r.fb.zcount.ensure(64)) return -1;
   if (rank == 0) {
@@ -132,13 +136,15 @@ void release_rank(Rank& r) {
   r.comm = nullptr;
   free_frame(r.fb);
   free_frame(r.rootfb);
-  for (DevBuf* b : {&r.frame, &r.ent, &r.rows, &r.small, &r.rows_all, &r.ent_all, &r.cin_ret,
+  for (DevBuf* b : {&r.frame, &r.ent, &r.rows, &r.small, &r.rows_all, &r.ent_all,
                     &r.frames_all, &r.small_all, &r.image})
     free_buf(*b);
   if (r.h_small) (void)hipHostFree(r.h_small);
   if (r.h_small_all) (void)hipHostFree(r.h_small_all);
   r.h_small = r.h_small_all = nullptr;
   for (auto& e : r.ev)
+    if (e) (void)hipEventDestroy(e);
+  for (auto& e : r.rev)
     if (e) (void)hipEventDestroy(e);
   if (r.ready) (void)hipEventDestroy(r.ready);
   if (r.stream) (void)hipStreamDestroy(r.stream);
@@ -217,59 +223,6 @@ int gather_var(rc_group& g, const std::vector<const void*>& send, void* recv,
   return 0;
 }
 
-// rank r's recv <- root.send[off[r] ..] (bytes[r] bytes)
-int scatter_var(rc_group& g, const void* send, const std::vector<void*>& recv,
-                const std::vector<size_t>& off, const std::vector<size_t>& bytes) {
-  if (g.transport == RC_XFER_RCCL) {
-    NCCL_TRY(ncclGroupStart());
-    for (size_t i = 0; i < g.ranks.size(); ++i) {
-      Rank& r = *g.ranks[i];
-      if (r.rank != 0) {
-        if (bytes[r.rank]) NCCL_TRY(ncclRecv(recv[i], bytes[r.rank], ncclUint8, 0, r.comm, r.stream));
-        continue;
-      }
-      for (int q = 1; q < g.nranks; ++q)
-        if (bytes[q])
-          NCCL_TRY(ncclSend((const char*)send + off[q], bytes[q], ncclUint8, q, r.comm, r.stream));
-    }
-    NCCL_TRY(ncclGroupEnd());
-    if (g.root && bytes[0]) {
-      HIP_TRY(hipSetDevice(g.root->device));
-      HIP_TRY(hipMemcpyAsync(recv[0], send, bytes[0], hipMemcpyDeviceToDevice, g.root->stream));
-    }
-    return 0;
-  }
-  Rank& root = *g.root;
-  HIP_TRY(hipSetDevice(root.device));
-  HIP_TRY(hipEventRecord(root.ready, root.stream));
-  for (size_t i = 0; i < g.ranks.size(); ++i) {
-    Rank& r = *g.ranks[i];
-    HIP_TRY(hipSetDevice(r.device));
-    if (&r != &root) HIP_TRY(hipStreamWaitEvent(r.stream, root.ready, 0));
-    if (bytes[r.rank])
-      HIP_TRY(hipMemcpyAsync(recv[i], (const char*)send + off[r.rank], bytes[r.rank],
-                             hipMemcpyDefault, r.stream));
-  }
-  return 0;
-}
-
-// rank r's recv <- root.send[r * bytes ..] (every rank receives `bytes`)
-int scatter_fixed(rc_group& g, const void* send, const std::vector<void*>& recv, size_t bytes) {
-  if (g.transport == RC_XFER_RCCL) {
-    NCCL_TRY(ncclGroupStart());
-    for (size_t i = 0; i < g.ranks.size(); ++i) {
-      Rank& r = *g.ranks[i];
-      NCCL_TRY(ncclScatter(r.rank == 0 ? send : nullptr, recv[i], bytes, ncclUint8, 0, r.comm,
-                           r.stream));
-    }
-    NCCL_TRY(ncclGroupEnd());
-    return 0;
-  }
-  std::vector<size_t> off(g.nranks), by(g.nranks, bytes);
-  for (int q = 0; q < g.nranks; ++q) off[q] = (size_t)q * bytes;
-  return scatter_var(g, send, recv, off, by);
-}
-
 int sync_all(rc_group& g) {
   for (auto& rp : g.ranks) {
     HIP_TRY(hipSetDevice(rp->device));
@@ -346,6 +299,14 @@ int render_one_rank(rc_group& g, const rc_scene* s, int W, int H, const rc_optio
 }
 
 // The whole sharded render; the caller holds every driven device's lock.
+//   fast:   every rank renders its rows; the row blocks are gathered and de-interleaved.
+//   parity: every rank runs phase A on its rows and packs its DEP entries (wire records with
+//           each entry's primary shade) and row summaries; the root gathers them and the row
+//           blocks (every non-DEP pixel is final after phase A) and de-interleaves the blocks
+//           into its image; it rebuilds the image's scan order in a lone frame's layout and
+//           runs a lone frame's resolver with phase C inside it, which shades every DEP entry
+//           into that image.  Nothing returns to the ranks: no carry-in scatter, no phase C on
+//           the ranks (round 3 did both, and gathered the row blocks only after phase C).
 int render_sharded(rc_group& g, const rc_scene* s, int W, int H, const rc_options* opt,
                    uint8_t* d_image, rc_timing* timing) {
   const auto t0 = std::chrono::steady_clock::now();
@@ -355,14 +316,17 @@ int render_sharded(rc_group& g, const rc_scene* s, int W, int H, const rc_option
   const bool parity = opt->mode == RC_MODE_PARITY && maxrec > 1;
   const size_t row_bytes = (size_t)W * 3;
   const size_t block_bytes = (size_t)rmax * row_bytes;
+  const size_t P = (size_t)W * H;
   Rank* root = g.root;
   if (G == 1 && root && tune().shard_lone)
     return render_one_rank(g, s, W, H, opt, d_image, timing, t0);
+  uint8_t* img = d_image;   // parity: the root's own image (P + 1 pixels: one spare)
   if (root) {
     HIP_TRY(hipSetDevice(root->device));
-    if (!d_image) {
-      if (root->image.ensure((size_t)H * row_bytes)) return -1;
-      d_image = (uint8_t*)root->image.p;
+    if (parity || !d_image) {
+      if (root->image.ensure((P + 1) * 3)) return -1;
+      img = (uint8_t*)root->image.p;
+      if (!d_image) d_image = img;
     }
     if (root->frames_all.ensure((size_t)G * block_bytes) || root->small_all.ensure((size_t)G * 16))
       return -1;
@@ -374,6 +338,7 @@ int render_sharded(rc_group& g, const rc_scene* s, int W, int H, const rc_option
   for (size_t i = 0; i < g.ranks.size(); ++i) {
     Rank& r = *g.ranks[i];
     HIP_TRY(hipSetDevice(r.device));
+    HIP_TRY(hipEventRecord(r.rev[0], r.stream));
     r.nrows = (H - r.rank + G - 1) / G;
     if (r.nrows < 0) r.nrows = 0;
     if (r.frame.ensure(block_bytes)) return -1;
@@ -384,10 +349,11 @@ int render_sharded(rc_group& g, const rc_scene* s, int W, int H, const rc_option
       if (r.nrows > 0)
         HIP_TRY(rc::launch_render(ls[i], W, H, r.rank, G, r.nrows, maxrec, (uint8_t*)r.frame.p,
                                   zc, r.stream, opt->mode == RC_MODE_CUDA));
+      HIP_TRY(hipEventRecord(r.rev[1], r.stream));
       continue;
     }
     // workspace for rmax rows on every rank: the fixed-size exchange moves the same number of
-    // entries (up to the bound, <= rmax * W) out of and into every rank's buffers
+    // entries (up to the bound, <= rmax * W) out of every rank's buffers
     if (ensure_parity(*r.c, r.fb, W, rmax, w[i], r.c->cus) ||
         r.ent.ensure((size_t)rmax * W * rc::shard_entry_bytes()) ||
         r.rows.ensure((size_t)rmax * rc::shard_row_bytes())) {
@@ -398,6 +364,7 @@ int render_sharded(rc_group& g, const rc_scene* s, int W, int H, const rc_option
                                    w[i], r.ent.p, r.rows.p, zc, r.stream));
     HIP_TRY(hipMemcpyAsync(r.small.p, w[i].counters + 2, sizeof(int), hipMemcpyDeviceToDevice,
                            r.stream));
+    HIP_TRY(hipEventRecord(r.rev[1], r.stream));
   }
   if (root) HIP_TRY(hipEventRecord(root->ev[1], root->stream));
   // fixed-size exchange when the last frame with this key bounds the entry counts; a bound
@@ -407,6 +374,7 @@ int render_sharded(rc_group& g, const rc_scene* s, int W, int H, const rc_option
                      g.bound.W == W && g.bound.H == H && g.bound.maxrec == maxrec;
   const long long per_rank = std::min<long long>(g.bound.per_rank, (long long)rmax * W);
   std::vector<size_t> cnt(G, 0);
+  std::vector<long long> offs(G, 0);
   if (parity) {
     // 2. row summaries and entry counts to the root
     std::vector<const void*> sr, sc;
@@ -418,7 +386,7 @@ int render_sharded(rc_group& g, const rc_scene* s, int W, int H, const rc_option
     if (gather_fixed(g, sr, root ? root->rows_all.p : nullptr, (size_t)rmax * rc::shard_row_bytes()) ||
         gather_fixed(g, sc, root ? root->small_all.p : nullptr, 16))
       return -1;
-    std::vector<size_t> off(G, 0), eb(G), eo(G), cb(G), co(G);
+    std::vector<size_t> off(G, 0), eb(G), eo(G);
     if (fixed) {   // every rank's list padded to the bound: sizes known without the counts
       for (int q = 0; q < G; ++q) cnt[q] = (size_t)per_rank;
     } else {   // the counts first (host synchronisation), then the exact sizes
@@ -437,66 +405,33 @@ int render_sharded(rc_group& g, const rc_scene* s, int W, int H, const rc_option
     size_t total = 0;
     for (int q = 0; q < G; ++q) {
       off[q] = total;
+      offs[q] = (long long)total;
       total += cnt[q];
     }
     for (int q = 0; q < G; ++q) {
       eb[q] = cnt[q] * rc::shard_entry_bytes();
       eo[q] = off[q] * rc::shard_entry_bytes();
-      cb[q] = cnt[q] * (size_t)rc::kCinBytes;
-      co[q] = off[q] * (size_t)rc::kCinBytes;
     }
-    // this frame's carry-in tag, the same on every rank (ranks render in lockstep)
-    g.epoch = g.epoch + 1 >= 0x80000000u ? 1 : g.epoch + 1;
-    // 3. the entries to the root, the resolver, the carry-ins back
-    rc::ParityWork wr{};
     if (root) {
       HIP_TRY(hipSetDevice(root->device));
-      root->rootfb.epoch = g.epoch - 1;
-      root->rootfb.scene_src = s->img;   // the resolver's evaluator is specialised by shape count
       // capacity for every rank's largest possible list (rmax * W): with the fixed-size
       // exchange a list longer than the bound is read (as garbage, the frame is rendered
       // again) beyond its block, never beyond the buffer
       const size_t cap = total > (size_t)G * rmax * W ? total : (size_t)G * rmax * W;
-      if (root->ent_all.ensure(cap * rc::shard_entry_bytes() + 64) ||
-          root->cin_ret.ensure(cap * (size_t)rc::kCinBytes + 64) ||
-          ensure_parity(*root->c, root->rootfb, W, H, wr, root->c->cus)) {
-        std::fprintf(stderr, "Error: out of device memory for the root's resolver workspace\n");
+      if (root->ent_all.ensure(cap * rc::shard_entry_bytes() + 64)) {
+        std::fprintf(stderr, "Error: out of device memory for the gathered DEP entries\n");
         return -1;
       }
-      if (root->rootfb.epoch != g.epoch) {   // ensure_parity cleared the tags on a wrap
-        g.epoch = root->rootfb.epoch;
-      }
     }
+    // 3. the entries to the root
     std::vector<const void*> se;
     for (auto& rp : g.ranks) se.push_back(rp->ent.p);
     if (fixed ? gather_fixed(g, se, root ? root->ent_all.p : nullptr, eb[0])
               : gather_var(g, se, root ? root->ent_all.p : nullptr, eo, eb))
       return -1;
-    if (root) {
-      HIP_TRY(hipSetDevice(root->device));
-      std::vector<long long> offs(off.begin(), off.end());
-      hipEvent_t rev[2] = {root->ev[2], root->ev[3]};
-      HIP_TRY(rc::launch_shard_resolve(ls[0], W, H, G, rmax, root->rows_all.p, root->ent_all.p,
-                                       offs.data(), maxrec, wr, root->cin_ret.p, root->stream,
-                                       rev, fixed ? (int)per_rank : 0x7fffffff));
-    }
-    std::vector<void*> rcv;
-    for (size_t i = 0; i < g.ranks.size(); ++i) rcv.push_back(w[i].cin);
-    if (fixed ? scatter_fixed(g, root ? root->cin_ret.p : nullptr, rcv, cb[0])
-              : scatter_var(g, root ? root->cin_ret.p : nullptr, rcv, co, cb))
-      return -1;
-    // 4. every rank: phase C of its entries
-    for (size_t i = 0; i < g.ranks.size(); ++i) {
-      Rank& r = *g.ranks[i];
-      if (!fixed && !r.ndep) continue;   // (fixed: the count is on the device only)
-      HIP_TRY(hipSetDevice(r.device));
-      HIP_TRY(rc::launch_shard_phase_c(ls[i], W, H, r.rank, G, maxrec, (uint8_t*)r.frame.p, w[i],
-                                       g.epoch, (unsigned long long*)r.fb.zcount.p, r.stream,
-                                       fixed ? (int)per_rank : 0x7fffffff));
-    }
   }
-  if (root) HIP_TRY(hipEventRecord(root->ev[4], root->stream));
-  // 5. the row blocks and the event counts to the root, the interleave undone there
+  // 4. the row blocks and the phase-A / render event counts to the root, the interleave undone
+  //    there (parity: into the root's image, ahead of the resolver; its DEP pixels follow)
   std::vector<const void*> sf, sz;
   for (auto& rp : g.ranks) {
     HIP_TRY(hipSetDevice(rp->device));
@@ -508,12 +443,60 @@ int render_sharded(rc_group& g, const rc_scene* s, int W, int H, const rc_option
   if (gather_fixed(g, sf, root ? root->frames_all.p : nullptr, block_bytes) ||
       gather_fixed(g, sz, root ? root->small_all.p : nullptr, 16))
     return -1;
+  for (auto& rp : g.ranks) {
+    HIP_TRY(hipSetDevice(rp->device));
+    HIP_TRY(hipEventRecord(rp->rev[2], rp->stream));
+  }
   if (root) {
     HIP_TRY(hipSetDevice(root->device));
-    HIP_TRY(rc::launch_deinterleave((const uint8_t*)root->frames_all.p, G, rmax, W, H, d_image,
-                                    root->stream));
+    HIP_TRY(rc::launch_deinterleave((const uint8_t*)root->frames_all.p, G, rmax, W, H,
+                                    parity ? img : d_image, root->stream));
+  }
+  // 5. parity, the root: the resolver with phase C inside it, into the root's image
+  unsigned long long* rz = nullptr;   // the root's phase C events
+  if (parity) {
+    // this frame's carry-in tag, the same on every rank (ranks render in lockstep)
+    g.epoch = g.epoch + 1 >= 0x80000000u ? 1 : g.epoch + 1;
+    if (root) {
+      rc::ParityWork wr{};
+      root->rootfb.epoch = g.epoch - 1;
+      root->rootfb.scene_src = s->img;   // the resolver's evaluator is specialised by shape count
+      // a lone frame's workspace over the whole image, plus the spare pixel P
+      if (ensure_parity(*root->c, root->rootfb, W, H, wr, root->c->cus, 0) ||
+          root->rootfb.deprec.ensure((P + 1) * rc::deprec_bytes()) ||
+          root->rootfb.wcarry.ensure((P + 1) * sizeof(float4)) || root->rootfb.zcount.ensure(64)) {
+        std::fprintf(stderr, "Error: out of device memory for the root's resolver workspace\n");
+        return -1;
+      }
+      if (root->rootfb.epoch != g.epoch)   // ensure_parity cleared the tags on a wrap
+        g.epoch = root->rootfb.epoch;
+      // ensure_parity's buffers may have been reallocated: the work's pointers are current
+      wr.deprec = root->rootfb.deprec.p;
+      wr.wcarry = (float4*)root->rootfb.wcarry.p;
+      wr.side = nullptr;
+      wr.split_shade = 0;
+      wr.patch = nullptr;
+      if (maxrec < 3) wr.inres = 0;   // a lone frame's schedule: phase C after at depth 1
+      rz = (unsigned long long*)root->rootfb.zcount.p;
+      HIP_TRY(hipMemsetAsync(rz, 0, sizeof(unsigned long long), root->stream));
+      hipEvent_t rev[2] = {root->ev[2], root->ev[3]};
+      HIP_TRY(rc::launch_shard_resolve(ls[0], W, H, G, rmax, root->rows_all.p, root->ent_all.p,
+                                       offs.data(), maxrec, wr, img, rz, root->stream, rev,
+                                       fixed ? (int)per_rank : 0x7fffffff));
+      HIP_TRY(hipEventRecord(root->ev[4], root->stream));
+      if (d_image != img)
+        HIP_TRY(hipMemcpyAsync(d_image, img, P * 3, hipMemcpyDeviceToDevice, root->stream));
+    }
+  } else if (root) {
+    HIP_TRY(hipEventRecord(root->ev[2], root->stream));
+    HIP_TRY(hipEventRecord(root->ev[3], root->stream));
+    HIP_TRY(hipEventRecord(root->ev[4], root->stream));
+  }
+  if (root) {
+    HIP_TRY(hipSetDevice(root->device));
     HIP_TRY(hipMemcpyAsync(root->h_small_all, root->small_all.p, (size_t)G * 16,
                            hipMemcpyDeviceToHost, root->stream));
+    if (rz) HIP_TRY(hipMemcpyAsync(root->h_small + 10, rz, 8, hipMemcpyDeviceToHost, root->stream));
     HIP_TRY(hipEventRecord(root->ev[5], root->stream));
   }
   if (parity) {
@@ -531,13 +514,13 @@ int render_sharded(rc_group& g, const rc_scene* s, int W, int H, const rc_option
       HIP_TRY(hipMemcpyAsync(rp->h_small, rp->small.p, 32, hipMemcpyDeviceToHost, rp->stream));
     }
   }
+  for (auto& rp : g.ranks) {
+    HIP_TRY(hipSetDevice(rp->device));
+    HIP_TRY(hipEventRecord(rp->rev[3], rp->stream));
+  }
   if (sync_all(g)) return -1;
   int rc = 0;
-  if (parity) {
-    for (auto& rp : g.ranks)
-      if (rp->fb.team.p && report_spin_error(rp->fb, "shard phase C")) rc = -1;
-    if (root && report_spin_error(root->rootfb, "shard resolver")) rc = -1;
-  }
+  if (parity && root && report_spin_error(root->rootfb, "shard resolver")) rc = -1;
   if (parity) {
     // the largest entry count of the frame (RCCL: the all-reduce; device copies: every rank is
     // in this process), identical on every rank
@@ -557,13 +540,22 @@ int render_sharded(rc_group& g, const rc_scene* s, int W, int H, const rc_option
     g.bound.maxrec = maxrec;
     g.bound.per_rank = mx;
   }
+  for (auto& rp : g.ranks) {   // every driven rank's own timeline
+    rc_rank_stats& q = rp->last;
+    std::memset(&q, 0, sizeof q);
+    q.rank = rp->rank;
+    q.local_ms = event_ms(rp->rev[0], rp->rev[1]);
+    q.exchange_ms = event_ms(rp->rev[1], rp->rev[2]);
+    q.total_ms = event_ms(rp->rev[0], rp->rev[3]);
+    q.rows = rp->nrows;
+    q.dep_pixels = parity ? rp->h_small[0] : 0;   // the rank's own DEP entries
+  }
   rc_shard_stats& st = g.last;
   std::memset(&st, 0, sizeof st);
   st.total_ms = ms_since(t0);
   if (root) {
     st.ranks = G;
     st.local_ms = event_ms(root->ev[0], root->ev[1]);
-    st.image_ms = event_ms(root->ev[4], root->ev[5]);
     st.device_ms = event_ms(root->ev[0], root->ev[5]);
     for (int q = 0; q < G; ++q) {
       long long z = 0;
@@ -572,12 +564,18 @@ int render_sharded(rc_group& g, const rc_scene* s, int W, int H, const rc_option
     }
     st.image_bytes = (long long)G * (long long)block_bytes;
     if (parity) {
+      long long z = 0;   // the root's phase C (inside its resolver)
+      std::memcpy(&z, root->h_small + 10, sizeof z);
+      st.zero_normalize += z;
       st.exchange_in_ms = event_ms(root->ev[1], root->ev[2]);
       st.resolve_ms = event_ms(root->ev[2], root->ev[3]);
       st.phase_c_ms = event_ms(root->ev[3], root->ev[4]);
+      st.image_ms = event_ms(root->ev[4], root->ev[5]);
       for (int q = 0; q < G; ++q) st.dep_pixels += root->h_small_all[4 * q];
       st.entry_bytes = st.dep_pixels * (long long)rc::shard_entry_bytes();
-      st.carry_bytes = st.dep_pixels * (long long)rc::kCinBytes;
+      st.carry_bytes = 0;
+    } else {
+      st.image_ms = event_ms(root->ev[1], root->ev[5]);
     }
   }
   if (timing) {
@@ -744,6 +742,16 @@ int rc_group_last_stats(const rc_group* g, rc_shard_stats* out) {
   if (!g || !out) return -1;
   *out = g->last;
   return 0;
+}
+
+int rc_group_rank_stats(const rc_group* g, int rank, rc_rank_stats* out) {
+  if (!g || !out) return -1;
+  for (auto& rp : g->ranks)
+    if (rp->rank == rank) {
+      *out = rp->last;
+      return 0;
+    }
+  return -1;   // this process does not drive that rank
 }
 
 }  // extern "C"

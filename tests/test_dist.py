@@ -8,10 +8,11 @@ for the kernels (test infrastructure).
   phase A on every rank (class, writer carry-outs, colours of the non-DEP pixels), the wire
   records (per DEP entry: image pixel, the last writer before it in its row and that writer's
   carry-out; per row: DEP count, segment starts inside the row, last writer / last DEP /
-  first DEP's writer and the last writer's carry-out) gathered to rank 0, which rebuilds the
-  image's scan order and segment table from them alone (k_shard_rows / k_row_scan /
-  k_shard_unpack), resolves the chain and scatters every rank its carry-ins; phase C on the
-  ranks; row blocks gathered.  The image must equal the oracle's whole-image render."""
+  first DEP's writer and the last writer's carry-out) and the row blocks gathered to rank 0,
+  which rebuilds the image's scan order and segment table from the records alone
+  (k_shard_rows / k_row_scan / k_shard_unpack), resolves the chain and shades every DEP entry
+  into the de-interleaved image itself (phase C inside the root's resolver); nothing returns
+  to the ranks.  The image must equal the oracle's whole-image render."""
 import ctypes
 import os
 import socket
@@ -151,27 +152,27 @@ def _worker(rank, world, port, name, W, H, depth, mode, result_path):
         local, entries, summaries, dep_pix, zero = rank_phase_a(scene, W, H, depth, rank, world)
         gathered = [None] * world if rank == 0 else None
         dist.gather_object((entries, summaries), gathered, dst=0)
-        cin_lists = None
-        if rank == 0:
-            cin_lists = root_resolve(scene, W, H, depth, world, [g[0] for g in gathered],
-                                     [g[1] for g in gathered])
-        mine = [None]
-        dist.scatter_object_list(mine, cin_lists, src=0)
-        cin = mine[0]
-        if len(entries):   # phase C on the rank
-            rgb, _, _, z = pixels(scene, W, H, depth, "parity", [e[0] for e in entries], cin)
-            for k, (j, x) in enumerate(dep_pix):
-                local[j, x] = rgb[k]
-            zero += int(z.sum())
-        send[:nrows] = torch.from_numpy(local)
+        send[:nrows] = torch.from_numpy(local)   # non-DEP pixels final after phase A
     blocks = [torch.empty_like(send) for _ in range(world)] if rank == 0 else None
     dist.gather(send, blocks, dst=0)
     zs = [None] * world if rank == 0 else None
     dist.gather_object(zero, zs, dst=0)
     if rank == 0:
         img = rc.deinterleave(torch.stack(blocks), H).numpy()
+        zero_all = sum(zs)
+        if mode == "parity":   # the root: the chain, then phase C of every DEP entry into img
+            ents = [g[0] for g in gathered]
+            cin = root_resolve(scene, W, H, depth, world, ents, [g[1] for g in gathered])
+            for g in range(world):
+                if not len(ents[g]):
+                    continue
+                pix = [e[0] for e in ents[g]]
+                rgb, _, _, z = pixels(scene, W, H, depth, "parity", pix, cin[g])
+                flat = img.reshape(-1, 3)
+                flat[np.asarray(pix)] = rgb
+                zero_all += int(z.sum())
         np.save(result_path, img)
-        np.save(result_path + ".zero.npy", np.array(sum(zs)))
+        np.save(result_path + ".zero.npy", np.array(zero_all))
     dist.destroy_process_group()
 
 

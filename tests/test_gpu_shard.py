@@ -1,8 +1,8 @@
 """GPU tests of the row-sharded path (rc_group / rc_render_sharded) through the
 C-ABI: rows dealt cyclically over G ranks, the root gathers the row blocks; in parity mode the
-root also gathers every rank's DEP entries, resolves the scan-order carry chain and returns the
-carry-ins for phase C on the ranks.  Every image must be byte-identical to the reference's
-(golden md5) or to the CPU oracle.
+root also gathers every rank's DEP entries (with their primary shades), resolves the scan-order
+carry chain and shades every DEP entry into its image (phase C inside its resolver).  Every
+image must be byte-identical to the reference's (golden md5) or to the CPU oracle.
 
 The box has one GPU, so G > 1 runs as G ranks on device 0 with device copies between their
 buffers (RC_XFER_COPY: the same kernels, wire records and exchange order as RCCL); the RCCL
@@ -166,15 +166,21 @@ def test_sharded_rccl_one_rank_exchange(mode, scenes, table):
 
 def test_sharded_repeat_and_stats(scenes, table):
     """Back-to-back sharded frames reuse every buffer (carry-in tags advance per frame); the
-    exchange volumes follow the wire formats (64 B per DEP entry in, 24 B carry-in back)."""
+    exchange volumes follow the wire format (80 B per DEP entry in, nothing back: phase C runs
+    on the root); every rank's own timeline is recorded (rc_group_rank_stats)."""
     key = "quadric:4096x4096:d6:parity"
     g4 = group([0] * 4, "copy")
     for _ in range(3):
         assert p3_md5(sharded(g4, scenes["quadric"], 4096, 4096, 6, "parity")) == table[key]["md5"]
     st = g4.stats()
     assert st["ranks"] == 4 and st["dep_pixels"] == 2804464
-    assert st["entry_bytes"] == 64 * st["dep_pixels"] and st["carry_bytes"] == 24 * st["dep_pixels"]
+    assert st["entry_bytes"] == 80 * st["dep_pixels"] and st["carry_bytes"] == 0
     assert st["resolve_ms"] > 0.0 and st["device_ms"] >= st["resolve_ms"]
+    ranks = [g4.rank_stats(r) for r in range(4)]
+    assert [q["rank"] for q in ranks] == [0, 1, 2, 3] and sum(q["rows"] for q in ranks) == 4096
+    assert sum(q["dep_pixels"] for q in ranks) == st["dep_pixels"]
+    assert all(q["local_ms"] > 0.0 and q["total_ms"] >= q["local_ms"] for q in ranks)
+    assert g4.rank_stats(4) is None
 
 
 @pytest.mark.parametrize("G", [2, 5])
