@@ -31,6 +31,10 @@
 // Which kernels use the cross-term-free quadric form (quad_x0: Scene::has_quadric == 2,
 // rc_device.hpp quad_abc) when the scene allows it.  A kernel with 0 folds has_quadric to 0/1,
 // so quad_x0 is a constant false there and the form and its branches are compiled out.
+#ifndef RC_EXP_NODEPW
+#define RC_EXP_NODEPW 0   // timing attribution build only (wrong images): phase A without its
+                          // DEP record and primary-shade stores
+#endif
 #ifndef RC_X0_PIXEL
 #define RC_X0_PIXEL 1     // k_render, k_phase_a, k_classify
 #endif
@@ -272,12 +276,12 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_
     if (RC_TILE_STAGE) ((uint8_t*)tb.cls[ly])[lx] = po.cls;
     else cls[p] = po.cls;
     if (po.cls == kClsDep) {
-      deprec[p] = po.dep;
+      if (!RC_EXP_NODEPW) deprec[p] = po.dep;
       // primary shade for phase C; this part's events are counted here (else phase C
       // recomputes the whole pixel and counts its events).  The pixel's framebuffer bytes
       // are phase C's: the tile writes a placeholder there.
       if (sc.dep_fast) {
-        wcarry[p] = make_float4(po.pcol.x, po.pcol.y, po.pcol.z, 0.0f);
+        if (!RC_EXP_NODEPW) wcarry[p] = make_float4(po.pcol.x, po.pcol.y, po.pcol.z, 0.0f);
         flush_events(zero, zcount);
       }
       if (RC_TILE_STAGE) tile_put_rgb(tb, lx, ly, 0, 0, 0, nullptr);

@@ -44,6 +44,8 @@ def main():
             for n in ("SQ_ACTIVE_INST_ANY", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY"):
                 if n in c:
                     e[n.lower().replace("sq_", "frac_")] = round(c[n] / wc, 4)
+        if c.get("SQ_THREAD_CYCLES_VALU") and c.get("SQ_ACTIVE_INST_VALU"):   # lanes per VALU op
+            e["valu_lane_util"] = round(c["SQ_THREAD_CYCLES_VALU"] / (64 * c["SQ_ACTIVE_INST_VALU"]), 4)
         if c.get("SQ_WAVES") and c.get("SQ_INSTS_VALU"):
             e["valu_insts_per_wave"] = round(c["SQ_INSTS_VALU"] / c["SQ_WAVES"])
         f64 = sum(c.get(f"SQ_INSTS_VALU_{o}_F64", 0) for o in ("ADD", "MUL", "FMA", "TRANS"))

@@ -45,4 +45,17 @@ if os.path.exists(path + ".waves"):
 for k in team:
     d = seg[k]
     if d.get("t0"):
-        print(f"team seg {k} starts at {((d['t0'] - base) & 0xffffffff) / 100:.1f} us")
+        print(f"team seg {k} starts at {(((d['t0'] - base + 2**31) & 0xffffffff) - 2**31) / 100:.1f} us")
+if os.path.exists(path + ".cyc"):   # helper items (dense runs handed off by regular waves)
+    for l in open(path + ".cyc"):
+        if not l.startswith("item"):
+            continue
+        f = l.split()
+        d = dict(zip(f[0::2], f[1::2]))
+        s = int(d["seg"])
+        t0 = ((int(d["t0"]) - base) & 0xffffffff) / 100.0
+        t1 = ((int(d["t1"]) - base) & 0xffffffff) / 100.0
+        st = ((seg[s].get("t0", base) - base) & 0xffffffff) / 100.0 if s in seg else float("nan")
+        print(f"helper item {d['item']}: seg {s} len {seg[s]['len'] if s in seg else '?'} "
+              f"seg start {st:.0f} us, handed off {t0:.0f} us, done {t1:.0f} us, "
+              f"{d['changers']} changers in {d['coop']} cooperative steps")
