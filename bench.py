@@ -84,6 +84,11 @@ PMC_PROFILES = {("quadric", 4096, 6, "parity"): "profiles/r03e_pmc_lone_4096.jso
 # differs from the lone frame's
 PMC_TRAFFIC_INFLIGHT = {("quadric", 4096, 6, "parity"): "profiles/r03f_pmc_traffic_inflight_4096.json"}
 
+# The headline's whole counter set from ONE command at HEAD (scripts/pmc_headline.sh: kernel
+# stats, VALU/wave-state and FETCH/WRITE passes of `bench.py --timed-only --steps 20 --warmup
+# 3`, the default frames in flight): valu_busy and traffic of the headline line come from it.
+PMC_HEADLINE = {("quadric", 4096, 6, "parity"): "profiles/r04_pmc_headline.json"}
+
 
 def pmc_kernel(kernel, scene, size, depth, mode, inflight=False):
     """Counter means of `kernel` from the committed PMC summary of this configuration:
@@ -108,6 +113,13 @@ def pmc_kernel(kernel, scene, size, depth, mode, inflight=False):
            "write_bytes": d["WRITE_SIZE"] * 1024 if "WRITE_SIZE" in d else None,
            "valu_busy": d.get("valu_busy")}
     if inflight:
+        hrel = PMC_HEADLINE.get((scene, size, depth, mode))
+        h = find(hrel)
+        if h is not None:   # one run: valu_busy and traffic of the frames-in-flight launches
+            return {"hbm_bytes": h.get("hbm_bytes"),
+                    "write_bytes": h["WRITE_SIZE"] * 1024 if "WRITE_SIZE" in h else None,
+                    "valu_busy": h.get("valu_busy"),
+                    "frac_wait_any": h.get("frac_wait_any")}, hrel
         trel = PMC_TRAFFIC_INFLIGHT.get((scene, size, depth, mode))
         t = find(trel)
         if t is not None:
@@ -339,7 +351,8 @@ def resolver_diag(d):
                           "lds_bytes": d["lds_bytes"], "team_blocks": d["team_blocks"]},
             "team_rounds_max": {"scan": d["scan_rounds_max"], "coop_scan": d["cscan_rounds_max"],
                                 "resolve": d["resolve_rounds_max"]},
-            "spin_wait_us_max": d["spin_wait_us_max"]}
+            "spin_wait_us_max": d["spin_wait_us_max"],
+            "clock_mhz": {"min": d["clock_mhz_min"], "max": d["clock_mhz_max"]}}
 
 
 def main():
@@ -639,6 +652,7 @@ def main():
                          "traffic": pmc["hbm_bytes"] if pmc else None,
                          "traffic_unit": "bytes per launch (HBM, PMC)",
                          "valu_busy": pmc["valu_busy"] if pmc else None,
+                         "frac_wait_any": pmc.get("frac_wait_any") if pmc else None,
                          "pmc_source": pmc_src,
                          "note": ("serial carry chain: latency-bound, see DESIGN.md; frac = per "
                                   "launch, frac_per_step = one image's work over ms_per_step"

@@ -222,7 +222,8 @@ int rc_pipe_reset(void);
  * placement needs would leave the grid partly queued behind resident workgroups; team rounds
  * = the most rounds of each kind one frame's team made; spin_wait_us_max[site] = the longest
  * bounded wait of any frame (sites: team hand-off, phase C carry-in, ready queue, helper
- * queue; waits under 10 us are not recorded). */
+ * queue; waits under 10 us are not recorded); clock_mhz_* = the shader clock each frame's
+ * resolver ran at (a throttled box explains a slow frame). */
 typedef struct rc_resolver_stats {
   int64_t frames;
   double resolve_ms_min, resolve_ms_max, resolve_ms_mean;
@@ -230,8 +231,10 @@ typedef struct rc_resolver_stats {
   int32_t regs, scratch_bytes, lds_bytes, team_blocks;
   int32_t scan_rounds_max, cscan_rounds_max, resolve_rounds_max, pad;
   double spin_wait_us_max[4];
+  int32_t clock_mhz_min, clock_mhz_max;   /* shader clock over each frame's resolver run
+                                             (s_memtime vs s_memrealtime in workgroup 0) */
 } rc_resolver_stats;
-_Static_assert(sizeof(rc_resolver_stats) == 112, "rc_resolver_stats layout (ctypes binding)");
+_Static_assert(sizeof(rc_resolver_stats) == 120, "rc_resolver_stats layout (ctypes binding)");
 int rc_resolver_stats_get(int lone, rc_resolver_stats *out);
 
 /* Duration (ms) of the last call's dominant kernel on the current device (the carry

@@ -107,7 +107,8 @@ class RcResolverStats(ctypes.Structure):
                 ("lds_bytes", ctypes.c_int32), ("team_blocks", ctypes.c_int32),
                 ("scan_rounds_max", ctypes.c_int32), ("cscan_rounds_max", ctypes.c_int32),
                 ("resolve_rounds_max", ctypes.c_int32), ("pad", ctypes.c_int32),
-                ("spin_wait_us_max", ctypes.c_double * 4)]
+                ("spin_wait_us_max", ctypes.c_double * 4),
+                ("clock_mhz_min", ctypes.c_int32), ("clock_mhz_max", ctypes.c_int32)]
 
 
 TUNING_FIELDS = ["side", "split_shade", "resolve_shared", "resolve_lds_kb", "resolve_grid",

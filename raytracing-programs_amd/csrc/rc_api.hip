@@ -134,6 +134,10 @@ long long FrameLog::poll() {
     diag.resolve_max = e->n_resolve > diag.resolve_max ? e->n_resolve : diag.resolve_max;
     for (int q = 0; q < 4; ++q)
       if (e->spin_ticks[q] > diag.spin_ticks_max[q]) diag.spin_ticks_max[q] = e->spin_ticks[q];
+    if (e->clock_mhz > 0) {
+      if (diag.clock_min == 0 || e->clock_mhz < diag.clock_min) diag.clock_min = e->clock_mhz;
+      if (e->clock_mhz > diag.clock_max) diag.clock_max = e->clock_mhz;
+    }
     e->code = kPending;
     ++tail;
     ++checked;
@@ -190,6 +194,8 @@ int fill_resolver_stats(DevCtx& c, const FrameLog::Diag& d, int grid, int res_cu
   r->cscan_rounds_max = d.cscan_max;
   r->resolve_rounds_max = d.resolve_max;
   for (int q = 0; q < 4; ++q) r->spin_wait_us_max[q] = d.spin_ticks_max[q] * 0.01;
+  r->clock_mhz_min = d.clock_min;
+  r->clock_mhz_max = d.clock_max;
   (void)c;
   return 0;
 }

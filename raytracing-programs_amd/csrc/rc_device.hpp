@@ -722,10 +722,15 @@ __device__ __forceinline__ uint8_t quant(float c) {
 }
 
 // State a first-bounce-miss (DEP) pixel carries from phase A to phases B/C.
-// A DEP pixel's transfer-function inputs (48 B).  Neither bounce direction below depends on
-// the carry, so phase A computes them once: `a` = level 2's direction
-// normalize(reflect(d1, n0)), and `b` = level 3's direction if level 2 also misses,
-// normalize(reflect(a, n0)) (C/raycast.c:349-350 with the stale normal of a miss).
+// A DEP pixel's transfer-function inputs.  Neither bounce direction below depends on the
+// carry, so phase A computes them once: `a` = level 2's direction normalize(reflect(d1, n0)),
+// and `b` = level 3's direction if level 2 also misses, normalize(reflect(a, n0))
+// (C/raycast.c:349-350 with the stale normal of a miss).  The record also holds the pixel's
+// primary shade (Scene::dep_fast, C/raycast.c:377), so phase A writes each DEP pixel as ONE
+// naturally aligned 64-byte line: the round-3 48-byte record plus a 16-byte shade slot beside
+// it cost partial-line writes (k_phase_a WRITE_SIZE 1.24x its algorithmic bytes in flight).
+// The resolver reads only the 48-byte record (its registers and LDS windows hold DepRec);
+// phase C reads the line.
 struct DepRec {
   float ax, ay, az;      // level-2 direction
   float n0x, n0y, n0z;   // primary normal (misses never update the normal)
@@ -734,12 +739,19 @@ struct DepRec {
   float bx, by, bz;      // level-3 direction when level 2 misses
   int pad2;
 };
+struct alignas(16) DepLine {   // 64-byte stride: pixel-indexed lines stay aligned
+  DepRec r;
+  float px, py, pz;      // primary shade (dep_fast; phase C's clean entries are exactly this)
+  int pad3;
+};
+static_assert(sizeof(DepRec) == 48 && sizeof(DepLine) == 64, "one 64-byte line per DEP pixel");
+__device__ __forceinline__ V3 dep_pcol(const DepLine* l) { return v3(l->px, l->py, l->pz); }
 
 struct PixelOut {
   V3 rgb;
   uint8_t cls;
   V3 carry;     // carry-out for writers (last bounce-hit point)
-  DepRec dep;
+  DepRec dep;   // DEP pixels
   V3 pcol;      // DEP pixels under dep_fast: the primary shade (C/raycast.c:377)
 };
 
@@ -816,13 +828,14 @@ __device__ __forceinline__ void shoot(const Scene& sc, V3 d, int maxrec, V3 carr
 
 // Phase C of a DEP pixel under dep_fast, from its carry-in c: the bounce loop of
 // iterative_shoot (C/raycast.c:348-376) resumed at level 2, then the primary shade phase A
-// computed (pcol, C/raycast.c:377-378).  Level 1 missed: its shade is the black phantom's
+// computed (the record's p*, C/raycast.c:377-378).  Level 1 missed: its shade is the black phantom's
 // (exactly zero), O = C = c, S = -1, N = N0, obj = obj0, T = refl[obj0]^2, and level 2's
 // direction normalize(reflect(D1, N0)) is the record's `a`.
-// The primary shade is read after the bounce loop (pcol: phase A's slot of the pixel), so it
-// does not stay live through it (register pressure: phase C spills).
-__device__ __forceinline__ V3 shade_dep_cont(const Scene& sc, const DepRec& r, int maxrec, V3 c,
-                                             const float4* __restrict__ pcol, int& zero_events) {
+// The primary shade is read from the record after the bounce loop, so it does not stay live
+// through it (register pressure: phase C spills).
+__device__ __forceinline__ V3 shade_dep_cont(const Scene& sc, const DepLine* __restrict__ rp,
+                                             int maxrec, V3 c, int& zero_events) {
+  const DepRec& r = rp->r;
   int obj = r.obj0, S = -1;
   const float T0 = sc.lshapes[obj].refl;
   float T = T0 * sc.lshapes[obj].refl;
@@ -845,7 +858,7 @@ __device__ __forceinline__ V3 shade_dep_cont(const Scene& sc, const DepRec& r, i
     O = C;
     S = i;
   }
-  const float4 k = *pcol;
+  const V3 k = dep_pcol(rp);
   return v3(out.x + k.x, out.y + k.y, out.z + k.z);
 }
 

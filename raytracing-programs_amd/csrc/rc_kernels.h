@@ -115,14 +115,16 @@ hipError_t launch_shard_local(const LaunchScene& s, int W, int H, int row0, int 
 // phase C tail, shading every DEP entry into `out` (W*H + 1 pixels; its non-DEP pixels are the
 // gathered row blocks).  ev (optional): [0] resolver start, [1] resolver end.  bound: entries
 // delivered per rank (the fixed-size exchange; beyond it a rank's list is not read as records).
+// ent0 (optional): rank 0's entries, read in place (the root's own list is not gathered).
 hipError_t launch_shard_resolve(const LaunchScene& s, int W, int H, int G, int rmax,
-                                const void* rows_all, const void* ent_all,
+                                const void* rows_all, const void* ent_all, const void* ent0,
                                 const long long* offs, int maxrec, const ParityWork& w,
                                 uint8_t* out, unsigned long long* zcount, hipStream_t stream,
                                 const hipEvent_t* ev, int bound = 0x7fffffff);
-// The root: image <- gathered row blocks [G][rmax][W*3].
-hipError_t launch_deinterleave(const uint8_t* gathered, int G, int rmax, int W, int H,
-                               uint8_t* img, hipStream_t stream);
+// The root: image <- gathered row blocks [G][rmax][W*3]; block0 (optional): rank 0's block in
+// place of gathered[0] (the root's own rows are not copied).
+hipError_t launch_deinterleave(const uint8_t* gathered, const uint8_t* block0, int G, int rmax,
+                               int W, int H, uint8_t* img, hipStream_t stream);
 
 size_t deprec_bytes();
 size_t row_stats_bytes();

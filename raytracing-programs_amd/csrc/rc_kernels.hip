@@ -67,6 +67,30 @@ constexpr int kTileW = RC_TILE_W, kTileH = 256 / RC_TILE_W;
 constexpr int kBlock = kTileW * kTileH;
 static_assert(kTileW % 8 == 0 && kTileH % 8 == 0, "8x8 wave tiles");
 
+// XCD-aware tile order (MI355X_MICROARCH.md: workgroups are dealt round-robin to the 8 XCDs,
+// each with its own L2).  With the grid's own order, horizontally adjacent tiles run on
+// different XCDs, so a 128-byte line of class bytes (8 tiles wide) or of framebuffer bytes
+// (~3 tiles) is written piecewise from several L2s and reaches HBM as partial-line writes
+// (rocprofv3 WRITE_SIZE of k_phase_a 1.26x its bytes).  Here XCD k takes the k-th contiguous
+// range of tiles in row-major order, so a line's tiles share one L2 and merge there.
+#ifndef RC_XCD_TILES
+#define RC_XCD_TILES 1
+#endif
+__device__ __forceinline__ void xcd_tile(int& bx, int& by) {
+  if (!RC_XCD_TILES) {
+    bx = blockIdx.x;
+    by = blockIdx.y;
+    return;
+  }
+  const int nx = gridDim.x, n = nx * (int)gridDim.y;
+  const int lin = (int)blockIdx.y * nx + (int)blockIdx.x;
+  const int xcd = lin & 7, k = lin >> 3, q = n >> 3, r = n & 7;
+  // XCDs below r take q + 1 tiles, the others q: a bijection of [0, n)
+  const int t = xcd < r ? xcd * (q + 1) + k : r * (q + 1) + (xcd - r) * q + k;
+  bx = t % nx;
+  by = t / nx;
+}
+
 __device__ __forceinline__ void tile_pixel(int& lx, int& ly) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   lx = (wave % (kTileW / 8)) * 8 + (lane & 7);
@@ -209,7 +233,9 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_
   if (!kStage) __syncthreads();
   int lx, ly;
   tile_pixel(lx, ly);
-  const int x0 = blockIdx.x * kTileW, r0 = blockIdx.y * kTileH;
+  int bx, by;
+  xcd_tile(bx, by);
+  const int x0 = bx * kTileW, r0 = by * kTileH;
   const int x = x0 + lx;
   const int r = r0 + ly;           // local (shard) row
   if (x < W && r < nrows) {
@@ -247,12 +273,33 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_
 }
 
 // ------------------------------------------------------------------ parity phase A --
+// A writer's carry-out is read only as a segment key: the last writer before a DEP pixel in
+// scan order (seg_init_carry), and by the row shards the last writer before a DEP pixel in its
+// row or the last writer of a row (k_shard_pack).  Inside the lane's 8-pixel row fragment of
+// the wave tile (lane = 8 * row + x), a writer followed by another writer with no DEP pixel
+// between them is neither, so phase A stores only the others: a writer with no later writer
+// in its fragment, or with a DEP pixel before the next one.  At quadric 4096^2 that drops most
+// of the 1.8 M sparse 16-byte stores (a few thousand keys are ever read).
+#ifndef RC_WKEY
+#define RC_WKEY 1   // 0: every writer stores its carry-out (round 3)
+#endif
+__device__ __forceinline__ bool writer_may_key(unsigned long long mw, unsigned long long md) {
+  if (!RC_WKEY) return true;
+  const int l = threadIdx.x & 63, fe = l | 7;
+  const unsigned long long upto = fe == 63 ? ~0ull : ((1ull << (fe + 1)) - 1ull);
+  const unsigned long long above = upto & ~((2ull << l) - 1ull);   // lanes l+1 .. fe (l = 63: none)
+  const unsigned long long nwm = mw & above;
+  if (!nwm) return true;
+  const int nw = __ffsll((long long)nwm) - 1;
+  return (md & above & ((1ull << nw) - 1ull)) != 0ull;
+}
+
 template <bool kStage>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_PHASE_A_WAVES))) k_phase_a(Scene sc, Cam cam, int W, int row0, int row_step, int nrows, int maxrec,
                                                     uint8_t* __restrict__ out,
                                                     uint8_t* __restrict__ cls,
                                                     float4* __restrict__ wcarry,
-                                                    DepRec* __restrict__ deprec,
+                                                    DepLine* __restrict__ deprec,
                                                     unsigned long long* __restrict__ zcount) {
   if (!RC_X0_PIXEL) sc.has_quadric = sc.has_quadric != 0;   // no cross-term-free form here (RC_X0_*)
   __shared__ StageBuf<kStage> stage;
@@ -264,7 +311,9 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_
   tile_pixel(lx, ly);
   // local row y (a shard renders rows row0 + y * row_step of the image; the whole image:
   // 0, 1, H); every per-pixel buffer is indexed by the local pixel
-  const int x0 = blockIdx.x * kTileW, y0 = blockIdx.y * kTileH;
+  int bx, by;
+  xcd_tile(bx, by);
+  const int x0 = bx * kTileW, y0 = by * kTileH;
   const int x = x0 + lx;
   const int y = y0 + ly;
   if (x < W && y < nrows) {
@@ -276,20 +325,24 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_
     if (RC_TILE_STAGE) ((uint8_t*)tb.cls[ly])[lx] = po.cls;
     else cls[p] = po.cls;
     if (po.cls == kClsDep) {
-      if (!RC_EXP_NODEPW) deprec[p] = po.dep;
-      // primary shade for phase C; this part's events are counted here (else phase C
-      // recomputes the whole pixel and counts its events).  The pixel's framebuffer bytes
-      // are phase C's: the tile writes a placeholder there.
-      if (sc.dep_fast) {
-        if (!RC_EXP_NODEPW) wcarry[p] = make_float4(po.pcol.x, po.pcol.y, po.pcol.z, 0.0f);
-        flush_events(zero, zcount);
+      // one 64-byte line: the record and, under dep_fast, the primary shade for phase C; this
+      // part's events are counted here (else phase C recomputes the whole pixel and counts its
+      // events).  The pixel's framebuffer bytes are phase C's: the tile writes a placeholder.
+      if (!RC_EXP_NODEPW) {
+        deprec[p].r = po.dep;
+        if (sc.dep_fast)
+          *(float4*)&deprec[p].px = make_float4(po.pcol.x, po.pcol.y, po.pcol.z, 0.0f);
       }
+      if (sc.dep_fast) flush_events(zero, zcount);
       if (RC_TILE_STAGE) tile_put_rgb(tb, lx, ly, 0, 0, 0, nullptr);
     } else {
-      if (po.cls == kClsWriter) wcarry[p] = make_float4(po.carry.x, po.carry.y, po.carry.z, 0.0f);
       tile_put_rgb(tb, lx, ly, quant(po.rgb.x), quant(po.rgb.y), quant(po.rgb.z), out + p * 3);
       flush_events(zero, zcount);
     }
+    const unsigned long long mw = __ballot(po.cls == kClsWriter);
+    const unsigned long long md = __ballot(po.cls == kClsDep);
+    if (po.cls == kClsWriter && writer_may_key(mw, md))
+      wcarry[p] = make_float4(po.carry.x, po.carry.y, po.carry.z, 0.0f);
   }
   if (!tile_last_wave(tb)) return;
   const int nx = W - x0 < kTileW ? W - x0 : kTileW;
@@ -305,7 +358,7 @@ template <bool kStage>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_PHASE_A_WAVES))) k_classify(Scene sc, Cam cam, int W, int H, int maxrec,
                                                      uint8_t* __restrict__ cls,
                                                      float4* __restrict__ wcarry,
-                                                     DepRec* __restrict__ deprec) {
+                                                     DepLine* __restrict__ deprec) {
   if (!RC_X0_PIXEL) sc.has_quadric = sc.has_quadric != 0;   // no cross-term-free form here (RC_X0_*)
   __shared__ StageBuf<kStage> stage;
   stage_scene<kStage>(sc, stage);
@@ -320,7 +373,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_
   PixelOut po;
   shoot<kModeClassify>(sc, d, maxrec, v3(0.0f, 0.0f, 0.0f), po, zero);
   cls[p] = po.cls;
-  if (po.cls == kClsDep) deprec[p] = po.dep;
+  if (po.cls == kClsDep) deprec[p].r = po.dep;
   else if (po.cls == kClsWriter) wcarry[p] = make_float4(po.carry.x, po.carry.y, po.carry.z, 0.0f);
 }
 
@@ -641,9 +694,9 @@ __device__ __forceinline__ V3 seg_init_carry(const long long* __restrict__ seg_k
 }
 
 // DEP entry j's record: phase A wrote it at the pixel (dep_pix[j]); gathered, never copied.
-__device__ __forceinline__ DepRec rec_at(const DepRec* __restrict__ deprec,
+__device__ __forceinline__ DepRec rec_at(const DepLine* __restrict__ deprec,
                                          const long long* __restrict__ dep_pix, int j) {
-  return deprec[dep_pix[j]];
+  return deprec[dep_pix[j]].r;   // the first 48 bytes of the line (the shade is phase C's)
 }
 
 // Resolve the 64 entries [base, base+64) ∩ [.., end) of one wave at carry `c`, changers
@@ -700,6 +753,14 @@ struct CarryHist {
 #define RC_PREDICT 1
 #endif
 constexpr bool kPredict = RC_PREDICT != 0;
+// Helper blocks' predictive step: 0 = its 15 guesses all for entry pos+1; k = groups 1..k guess
+// pos+1 and groups k+1..15 guess pos+2 (oracle simulation of the seven dense 1 377-entry
+// segments at quadric 4096^2, scripts/pred_sim.py: 1.65-1.99 entries per step with 15/0,
+// 1.54-2.95 with 7/8, 1.60-2.91 with 9/6)
+#ifndef RC_PRED_SPLIT
+#define RC_PRED_SPLIT 0
+#endif
+constexpr int kPredSplit = RC_PRED_SPLIT;
 __device__ __forceinline__ void hist_push(CarryHist& hs, V3 c) {
   hs.run = hs.n == 0 ? 0 : hs.run + 1;
   hs.h[3] = hs.h[2];
@@ -710,7 +771,7 @@ __device__ __forceinline__ void hist_push(CarryHist& hs, V3 c) {
 }
 // guess q (1..) of the carry after c: the mean delta of the history, in float bits, with the
 // moving component offset by 0, -1, +1, -2, +2, ...
-__device__ __forceinline__ V3 hist_guess(const CarryHist& hs, V3 c, int q) {
+__device__ __forceinline__ V3 hist_guess(const CarryHist& hs, V3 c, int q, int mult = 1) {
   // no run-time index into h[] (it would put the history in scratch memory, whose reload
   // waits for every store in flight — the carry-in publications) and no run-time divisor
   const int m = hs.n - 1;   // 1..3
@@ -721,6 +782,7 @@ __device__ __forceinline__ V3 hist_guess(const CarryHist& hs, V3 c, int q) {
     return m == 1 ? d : (m == 2 ? (d + r) / 2 : (d + r) / 3);
   };
   int dx = md(hs.h[0].x, o.x), dy = md(hs.h[0].y, o.y), dz = md(hs.h[0].z, o.z);
+  if (mult != 1) dx *= mult, dy *= mult, dz *= mult;
   const int j = q - 1;
   const int off = (j & 1) ? -((j + 1) >> 1) : (j >> 1);   // q = 1, 2, 3, 4.. -> 0, -1, +1, -2..
   const int ax = abs(dx), ay = abs(dy), az = abs(dz);
@@ -733,7 +795,7 @@ __device__ __forceinline__ V3 hist_guess(const CarryHist& hs, V3 c, int q) {
 }
 
 __device__ __forceinline__ int wave_window(const Scene& sc, int maxrec,
-                                           const DepRec* __restrict__ deprec,
+                                           const DepLine* __restrict__ deprec,
                                            const long long* __restrict__ dep_pix, int base,
                                            int end, V3& c, V3& mine, bool& mhit,
                                            const LaneShape& ls,
@@ -1141,9 +1203,14 @@ __device__ __forceinline__ int block_window(const Scene& sc, int maxrec, BlockWi
     if (coop && hp && kPredict && hp->n >= 2 && pos + 1 < nvalid && Eb <= 16 && Eb >= 2) {
       ++ws.coop;
       const int gi = wave * E + e;
-      const int i = pos + (gi > 0 ? 1 : 0);
-      const V3 ce = sel(gi > 0, hist_guess(*hp, c, gi), c);
-      const DepRec ri = bw.rec[i];
+      // groups 1..k1 guess entry pos+1's carry-in; with RC_PRED_SPLIT the groups above k1 guess
+      // entry pos+2's (twice the history's mean step: a hit retires three entries)
+      const bool three = kPredSplit > 0 && kPredSplit < Eb - 1 && pos + 2 < nvalid;
+      const int k1 = three ? kPredSplit : Eb - 1;
+      const bool g2 = gi > k1;
+      const int i = pos + (gi > 0 ? 1 : 0) + (g2 ? 1 : 0);
+      const V3 ce = sel(gi > 0, hist_guess(*hp, c, g2 ? gi - k1 : gi, g2 ? 2 : 1), c);
+      const DepRec ri = bw.rec[i < nvalid ? i : pos];
       V3 oc = ce;
       bool hg = false;
 #if RC_STAMPS
@@ -1184,9 +1251,9 @@ __device__ __forceinline__ int block_window(const Scene& sc, int maxrec, BlockWi
       ws.cw += __builtin_amdgcn_s_memtime() - bw0_;
 #endif
       const V3 o0 = v3(bw.pout[par][0][0], bw.pout[par][0][1], bw.pout[par][0][2]);
-      const bool mt = lane > 0 && lane < Eb &&
-                      same_bits(v3(bw.pce[par][lane][0], bw.pce[par][lane][1],
-                                   bw.pce[par][lane][2]), o0);
+      const V3 pl = v3(bw.pce[par][lane < Eb ? lane : 0][0], bw.pce[par][lane < Eb ? lane : 0][1],
+                       bw.pce[par][lane < Eb ? lane : 0][2]);
+      const bool mt = lane > 0 && lane <= k1 && same_bits(pl, o0);
       const unsigned long long mm = __ballot(mt);
       const int mi = mm ? __ffsll((long long)mm) - 1 : 0;
       if (t == pos) cin_put(cin, base + pos, c, tag, bw.phit[par][0] != 0);
@@ -1210,6 +1277,21 @@ __device__ __forceinline__ int block_window(const Scene& sc, int maxrec, BlockWi
             ++ws.changers;
             hist_push(*hp, o1);
             c = o1;
+            // entry pos+2 (now pos) evaluated at a guess equal to o1: its exact evaluation
+            const unsigned long long m2 = three ? __ballot(lane > k1 && lane < Eb && same_bits(pl, o1)) : 0ull;
+            if (m2) {
+              const int mj = __ffsll((long long)m2) - 1;
+              const V3 o2 = v3(bw.pout[par][mj][0], bw.pout[par][mj][1], bw.pout[par][mj][2]);
+              if (t == pos) cin_put(cin, base + pos, o1, tag, bw.phit[par][mj] != 0);
+              pos += 1;
+              if (same_bits(o2, o1)) {
+                hp->n = 0;
+              } else {
+                ++ws.changers;
+                hist_push(*hp, o2);
+                c = o2;
+              }
+            }
           }
         } else {
           c = o0;
@@ -1382,7 +1464,10 @@ struct TeamState {
   // longest bounded wait of the frame in 10 ns ticks (waits under 10 us are not noted)
   int n_scan, n_cscan, n_resolve;
   int spin_ticks[4];
-  int pad[18];
+  // the shader clock over the resolver's own run (workgroup 0: s_memtime cycles per 10 ns tick
+  // of s_memrealtime, in MHz): a throttled box shows here instead of as an unexplained slow step
+  int clock_mhz;
+  int pad[17];
   TeamSlot slot[2][kTeamMax];
   DenseQueue dq;
 };
@@ -1390,7 +1475,7 @@ struct TeamState {
 static_assert(sizeof(TeamState) % 16 == 0, "k_row_stats clears TeamState in 16-byte words");
 // the host's per-frame record (rc_runtime.h FrameLog::Entry) is TeamState's first 64 bytes
 static_assert(offsetof(TeamState, n_scan) == 28 && offsetof(TeamState, spin_ticks) == 40 &&
-                  offsetof(TeamState, pad) == 56,
+                  offsetof(TeamState, clock_mhz) == 56 && offsetof(TeamState, pad) == 60,
               "FrameLog::Entry layout");
 
 // spin sites (TeamState::spin_ticks)
@@ -1565,8 +1650,7 @@ __device__ __forceinline__ bool batch_carries(CinG* cin, int ndep, int b, unsign
 // the others resume at level 2 (shade_dep_cont).  Otherwise the pixel is recomputed.
 __device__ __forceinline__ void shade_batch(const Scene& sc, const Cam& cam, int W, int maxrec,
                                             const long long* __restrict__ dep_pix,
-                                            const DepRec* __restrict__ deprec,
-                                            const float4* __restrict__ pcol, int ndep, int b,
+                                            const DepLine* __restrict__ deprec, int ndep, int b,
                                             V3 c, bool hit, uint8_t* __restrict__ out,
                                             uint32_t* __restrict__ patch, int& zero) {
   const int j = b * 64 + (int)(threadIdx.x & 63);
@@ -1575,10 +1659,9 @@ __device__ __forceinline__ void shade_batch(const Scene& sc, const Cam& cam, int
   if (sc.dep_fast) {
     V3 rgb;
     if (hit) {
-      rgb = shade_dep_cont(sc, deprec[p], maxrec, c, pcol + p, zero);
+      rgb = shade_dep_cont(sc, deprec + p, maxrec, c, zero);
     } else {
-      const float4 k = pcol[p];
-      rgb = v3(k.x, k.y, k.z);
+      rgb = dep_pcol(deprec + p);
     }
     store_dep(out, patch, p, j, rgb);
     return;
@@ -1615,8 +1698,7 @@ __device__ __forceinline__ void shade_tile(const Scene& sc, const Cam& cam, int 
 // Phase C pass 1 (published batches) and pass 2 (everything unclaimed, waiting).
 __device__ __forceinline__ void phase_c_passes(const Scene& sc, const Cam& cam, int W,
                                                int maxrec, const long long* __restrict__ dep_pix,
-                                               const DepRec* __restrict__ deprec,
-                                               const float4* __restrict__ pcol,
+                                               const DepLine* __restrict__ deprec,
                                                CinG* __restrict__ cin, int* __restrict__ counters,
                                                int* __restrict__ batch_state,
                                                uint8_t* __restrict__ out,
@@ -1643,7 +1725,7 @@ __device__ __forceinline__ void phase_c_passes(const Scene& sc, const Cam& cam, 
     int mine = 0;
     if ((threadIdx.x & 63) == 0) mine = batch_claim(batch_state, b);
     if (!__shfl(mine, 0, 64)) continue;
-    shade_batch(sc, cam, W, maxrec, dep_pix, deprec, pcol, ndep, b, c, hit, out, patch, zero);
+    shade_batch(sc, cam, W, maxrec, dep_pix, deprec, ndep, b, c, hit, out, patch, zero);
     if ((threadIdx.x & 63) == 0) atomicAdd(done_ctr, 1);
   }
   for (;;) {
@@ -1655,7 +1737,7 @@ __device__ __forceinline__ void phase_c_passes(const Scene& sc, const Cam& cam, 
     V3 c = v3(0.0f, 0.0f, 0.0f);
     bool hit = true;
     (void)batch_carries(cin, ndep, b, tag, true, c, hit, ts);
-    shade_batch(sc, cam, W, maxrec, dep_pix, deprec, pcol, ndep, b, c, hit, out, patch, zero);
+    shade_batch(sc, cam, W, maxrec, dep_pix, deprec, ndep, b, c, hit, out, patch, zero);
     if ((threadIdx.x & 63) == 0) atomicAdd(done_ctr, 1);
   }
 }
@@ -1667,8 +1749,7 @@ __device__ __forceinline__ void phase_c_passes(const Scene& sc, const Cam& cam, 
 // k_finish takes whatever these waves have not claimed.
 __device__ __forceinline__ void phase_c_ready(const Scene& sc, const Cam& cam, int W,
                                               int maxrec, const long long* __restrict__ dep_pix,
-                                              const DepRec* __restrict__ deprec,
-                                              const float4* __restrict__ pcol,
+                                              const DepLine* __restrict__ deprec,
                                               CinG* __restrict__ cin, int* __restrict__ counters,
                                               int* __restrict__ batch_state,
                                               const int* __restrict__ rq, uint8_t* __restrict__ out,
@@ -1726,7 +1807,7 @@ __device__ __forceinline__ void phase_c_ready(const Scene& sc, const Cam& cam, i
     bool hit = true;
     if (tq && (threadIdx.x & 63) == 0) tq[3 * k + 1] = (unsigned)__builtin_amdgcn_s_memrealtime();
     (void)batch_carries(cin, ndep, b, tag, true, c, hit, ts);   // published: arrives at once
-    shade_batch(sc, cam, W, maxrec, dep_pix, deprec, pcol, ndep, b, c, hit, out, patch, zero);
+    shade_batch(sc, cam, W, maxrec, dep_pix, deprec, ndep, b, c, hit, out, patch, zero);
     if ((threadIdx.x & 63) == 0) atomicAdd(&counters[9], 1);
     if (tq && (threadIdx.x & 63) == 0) tq[3 * k + 2] = (unsigned)__builtin_amdgcn_s_memrealtime();
   }
@@ -1737,8 +1818,7 @@ __device__ __forceinline__ void phase_c_ready(const Scene& sc, const Cam& cam, i
 // instead of leaving its SIMD idle; k_finish, after the resolver, finds the queue drained.
 __device__ __forceinline__ void resolver_phase_c(const Scene& sc, const Cam& cam, int W, int maxrec,
                                               const long long* __restrict__ dep_pix,
-                                              const DepRec* __restrict__ deprec,
-                                              const float4* __restrict__ pcol,
+                                              const DepLine* __restrict__ deprec,
                                               CinG* __restrict__ cin, int* __restrict__ counters,
                                               int* __restrict__ batch_state,
                                               const int* __restrict__ rq,
@@ -1749,7 +1829,7 @@ __device__ __forceinline__ void resolver_phase_c(const Scene& sc, const Cam& cam
                                               int helpers) {
   int zero = 0;
   const int waves = ((int)gridDim.x - helpers) * (kResolveBlock / 64);
-  phase_c_ready(sc, cam, W, maxrec, dep_pix, deprec, pcol, cin, counters, batch_state, rq, out,
+  phase_c_ready(sc, cam, W, maxrec, dep_pix, deprec, cin, counters, batch_state, rq, out,
                 patch, ts, tag, zero, nullptr, mode == 2 ? waves : 0, helpers);
   flush_events(zero, zcount);
 }
@@ -1758,7 +1838,7 @@ __device__ __forceinline__ void resolver_phase_c(const Scene& sc, const Cam& cam
 // SIMD each), so the kernel must stay within 256 registers (VGPRs + AGPRs) per wave
 template <bool kLds>
 __global__ void __launch_bounds__(kResolveBlock) __attribute__((amdgpu_waves_per_eu(2))) k_resolve(
-    Scene sc, int maxrec, const DepRec* __restrict__ deprec,
+    Scene sc, int maxrec, const DepLine* __restrict__ deprec,
     const long long* __restrict__ dep_pix, const long long* __restrict__ seg_key,
     const float4* __restrict__ wcarry,
     const int* __restrict__ seg_start, const int* __restrict__ seg_order,
@@ -1772,6 +1852,8 @@ __global__ void __launch_bounds__(kResolveBlock) __attribute__((amdgpu_waves_per
   if (!RC_X0_RESOLVE) sc.has_quadric = sc.has_quadric != 0;   // no cross-term-free form here (RC_X0_*)
   // the product build has no trace: its timestamps and counters then hold no registers
   if (!RC_DIAG) trace = nullptr;
+  const unsigned long long clk_t0 = __builtin_amdgcn_s_memrealtime();
+  const unsigned long long clk_c0 = __builtin_amdgcn_s_memtime();
   // census for phase C's side kernel: it only proceeds once every resolver block is resident
   if (threadIdx.x == 0)
     __hip_atomic_fetch_add(&counters[5], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2224,7 +2306,7 @@ __global__ void __launch_bounds__(kResolveBlock) __attribute__((amdgpu_waves_per
     if (inres) {
       if (threadIdx.x == 0)
         __hip_atomic_fetch_add(&ts->helpers_out, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      resolver_phase_c(sc, cam, W, maxrec, dep_pix, deprec, wcarry, cin, counters, batch_state,
+      resolver_phase_c(sc, cam, W, maxrec, dep_pix, deprec, cin, counters, batch_state,
                        rq, out, patch, zcount, ts, tag, inres, helpers);
     }
     return;   // helpers take no regular segments
@@ -2408,17 +2490,22 @@ __global__ void __launch_bounds__(kResolveBlock) __attribute__((amdgpu_waves_per
   // this wave hands nothing off any more (helper blocks wait for every such wave)
   if (lane == 0)
     __hip_atomic_fetch_add(&ts->dq.finished, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {   // the frame's record: shader clock of this run
+    const unsigned long long dt = __builtin_amdgcn_s_memrealtime() - clk_t0;
+    const unsigned long long dc = __builtin_amdgcn_s_memtime() - clk_c0;
+    if (dt > 0) ts->clock_mhz = (int)(dc * 100ull / dt);
+  }
   if (trace && lane == 0)   // debug trace: when each wave leaves
     trace[3 * (size_t)ndep + 5 * (size_t)nseg + 8 * 8192 + blockIdx.x * 4 + wave] =
         (unsigned)__builtin_amdgcn_s_memrealtime();
-  if (inres) resolver_phase_c(sc, cam, W, maxrec, dep_pix, deprec, wcarry, cin, counters,
+  if (inres) resolver_phase_c(sc, cam, W, maxrec, dep_pix, deprec, cin, counters,
                               batch_state, rq, out, patch, zcount, ts, tag, inres, helpers);
 }
 template <bool kStage>
 __global__ void __launch_bounds__(kSideBlock) k_side(
     Scene sc, Cam cam, int W, int H, int maxrec, const uint8_t* __restrict__ cls,
-    const long long* __restrict__ dep_pix, const DepRec* __restrict__ deprec,
-    const float4* __restrict__ pcol, CinG* __restrict__ cin, int* __restrict__ counters,
+    const long long* __restrict__ dep_pix, const DepLine* __restrict__ deprec,
+    CinG* __restrict__ cin, int* __restrict__ counters,
     int* __restrict__ batch_state, const int* __restrict__ rq, uint8_t* __restrict__ out,
     uint32_t* __restrict__ patch, unsigned long long* __restrict__ zcount,
     TeamState* __restrict__ ts, int resolve_blocks, unsigned tag, int tiles,
@@ -2458,7 +2545,7 @@ __global__ void __launch_bounds__(kSideBlock) k_side(
     shade_tile(sc, cam, W, H, maxrec, t, cls, out, zero);
     if ((threadIdx.x & 63) == 0) atomicAdd(&counters[8], 1);
   }
-  phase_c_ready(sc, cam, W, maxrec, dep_pix, deprec, pcol, cin, counters, batch_state, rq, out,
+  phase_c_ready(sc, cam, W, maxrec, dep_pix, deprec, cin, counters, batch_state, rq, out,
                 patch, ts, tag, zero, trace);
   flush_events(zero, zcount);
 }
@@ -2470,8 +2557,8 @@ __global__ void __launch_bounds__(kSideBlock) k_side(
 template <bool kStage>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_FINISH_WAVES))) k_finish(
     Scene sc, Cam cam, int W, int H, int maxrec, const uint8_t* __restrict__ cls,
-    const long long* __restrict__ dep_pix, const DepRec* __restrict__ deprec,
-    const float4* __restrict__ pcol, CinG* __restrict__ cin, int* __restrict__ counters,
+    const long long* __restrict__ dep_pix, const DepLine* __restrict__ deprec,
+    CinG* __restrict__ cin, int* __restrict__ counters,
     int* __restrict__ batch_state, uint8_t* __restrict__ out, uint32_t* __restrict__ patch,
     unsigned long long* __restrict__ zcount, TeamState* __restrict__ ts, unsigned tag,
     int tiles, const int* __restrict__ rq) {
@@ -2496,9 +2583,9 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_
   // kernel runs: the last ones are the resolver's final rounds, shaded here at full occupancy
   // instead of by k_side's one workgroup per CU), then anything still unclaimed
   if (rq)
-    phase_c_ready(sc, cam, W, maxrec, dep_pix, deprec, pcol, cin, counters, batch_state, rq,
+    phase_c_ready(sc, cam, W, maxrec, dep_pix, deprec, cin, counters, batch_state, rq,
                   out, patch, ts, tag, zero, nullptr);
-  phase_c_passes(sc, cam, W, maxrec, dep_pix, deprec, pcol, cin, counters, batch_state, out, patch, ts, tag, false,
+  phase_c_passes(sc, cam, W, maxrec, dep_pix, deprec, cin, counters, batch_state, out, patch, ts, tag, false,
                  zero);
   flush_events(zero, zcount);
 }
@@ -2522,7 +2609,7 @@ template <bool kStage, bool kFast>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_FINISH_WAVES))) k_dep_chunks(
     Scene sc, Cam cam, int W, int row0, int row_step, int maxrec,
     const long long* __restrict__ dep_pix,
-    const DepRec* __restrict__ deprec, const float4* __restrict__ pcol, CinG* __restrict__ cin,
+    const DepLine* __restrict__ deprec, CinG* __restrict__ cin,
     const int* __restrict__ counters, uint8_t* __restrict__ out, uint32_t* __restrict__ patch,
     unsigned long long* __restrict__ zcount, TeamState* __restrict__ ts, unsigned tag,
     int limit) {
@@ -2552,8 +2639,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_
       const bool hv = in && (!kFast || hit);
       if (in && !hv) {
         const long long p = dep_pix[j];
-        const float4 k = pcol[p];
-        store_dep(out, patch, p, j, v3(k.x, k.y, k.z));
+        store_dep(out, patch, p, j, dep_pcol(deprec + p));
       }
       const unsigned long long m = __ballot(hv);
       int base = 0;
@@ -2575,7 +2661,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_
       const long long p = dep_pix[j];
       V3 rgb;
       if constexpr (kFast) {
-        rgb = shade_dep_cont(sc, deprec[p], maxrec, c, pcol + p, zero);
+        rgb = shade_dep_cont(sc, deprec + p, maxrec, c, zero);
       } else {
         const int y = row0 + (int)(p / W) * row_step, x = (int)(p % W);   // p: local pixel
         const V3 d = primary_dir(cam, x, y, zero);
@@ -2604,9 +2690,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_
 // fields in image pixel indices, the row's first entry in the rank's list and the carry-out of
 // the row's last writer (the key of a segment that starts after this row).
 struct ShardEntry {
-  DepRec rec;
+  DepLine rec;   // with the entry's primary shade (phase A, Scene::dep_fast): phase C runs on the root
   float4 kc;     // carry-out of the last writer before the entry in its row
-  float4 pcol;   // the entry's primary shade (phase A, Scene::dep_fast): phase C runs on the root
 };
 struct RowShard {
   int ndep, nstart, loff, pad;
@@ -2619,7 +2704,7 @@ static_assert(sizeof(ShardEntry) == 80 && sizeof(RowShard) == 64, "wire records"
 // entries (at the local DEP offsets of k_row_scan) and the row summary.
 __global__ void __launch_bounds__(256) k_shard_pack(
     const uint8_t* __restrict__ cls, const float4* __restrict__ wcarry,
-    const DepRec* __restrict__ deprec, int W, int row0, int row_step, int nrows,
+    const DepLine* __restrict__ deprec, int W, int row0, int row_step, int nrows,
     const int* __restrict__ row_off, long long* __restrict__ dep_pix,
     ShardEntry* __restrict__ ent, RowShard* __restrict__ rs) {
   const int y = blockIdx.x * kRowWaves + (int)(threadIdx.x >> 6);
@@ -2650,10 +2735,9 @@ __global__ void __launch_bounds__(256) k_shard_pack(
       dep_pix[l] = lbase + x;
       ShardEntry e;
       e.rec = deprec[lbase + x];
-      e.rec.pad = (int)(gbase + x);
-      e.rec.pad2 = kw >= 0 ? (int)(gbase + kw) : -1;
+      e.rec.r.pad = (int)(gbase + x);
+      e.rec.r.pad2 = kw >= 0 ? (int)(gbase + kw) : -1;
       e.kc = kw >= 0 ? wcarry[lbase + kw] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-      e.pcol = wcarry[lbase + x];   // a DEP pixel's slot: its primary shade (dep_fast)
       ent[l] = e;
     }
     l0 += __popcll(md);
@@ -2696,10 +2780,11 @@ __global__ void __launch_bounds__(256) k_shard_rows(const RowShard* __restrict__
 // framebuffer stores then run exactly as in a lone frame, into the root's image.  A segment
 // start is decided exactly as in k_row_compact (writer after the previous DEP).
 __global__ void __launch_bounds__(256) k_shard_unpack(
-    const RowShard* __restrict__ rsall, const ShardEntry* __restrict__ ent, ShardOffs offs,
+    const RowShard* __restrict__ rsall, const ShardEntry* __restrict__ ent,
+    const ShardEntry* __restrict__ ent0, ShardOffs offs,
     int G, int rmax, int W, int H, const int* __restrict__ row_off,
     const int* __restrict__ row_soff, const long long* __restrict__ row_prevw,
-    const long long* __restrict__ row_prevd, DepRec* __restrict__ deprec,
+    const long long* __restrict__ row_prevd, DepLine* __restrict__ deprec,
     long long* __restrict__ dep_pix, int* __restrict__ seg_start,
     long long* __restrict__ seg_key, float4* __restrict__ wcarry, int bound) {
   const int y = blockIdx.x * kRowWaves + (int)(threadIdx.x >> 6);
@@ -2708,7 +2793,8 @@ __global__ void __launch_bounds__(256) k_shard_unpack(
   const long long P = (long long)W * H;
   const int g = y % G;
   const RowShard r = rsall[(size_t)g * rmax + y / G];
-  const ShardEntry* e = ent + offs.off[g] + r.loff;
+  // rank 0's entries are the root's own list (never copied), the others' the gathered blocks
+  const ShardEntry* e = (g == 0 && ent0 ? ent0 : ent + offs.off[g]) + r.loff;
   const int n = r.ndep;
   const int idx0 = row_off[y];
   int s0 = row_soff[y];
@@ -2730,15 +2816,15 @@ __global__ void __launch_bounds__(256) k_shard_unpack(
     // an entry becomes a harmless record (zero directions, shape 0) at the spare pixel P (the
     // root's buffers hold P + 1 pixels), continuing its segment — never an out-of-range shape
     // or pixel index for the resolver and phase C
-    const bool spare = valid && (r.loff + i >= bound || q.rec.pad < 0 || q.rec.pad >= P);
+    const bool spare = valid && (r.loff + i >= bound || q.rec.r.pad < 0 || q.rec.r.pad >= P);
     if (spare) {
-      q.rec = DepRec{0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0, -1, 0.0f, 0.0f, 0.0f, -1};
+      q.rec = DepLine{DepRec{0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0, -1, 0.0f, 0.0f, 0.0f, -1},
+                      0.0f, 0.0f, 0.0f, 0};
       q.kc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-      q.pcol = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     }
-    const long long pix = valid ? (spare ? P : (long long)q.rec.pad) : -1;
-    const long long kin = valid && !spare && q.rec.pad2 >= 0 && q.rec.pad2 < P
-                              ? (long long)q.rec.pad2 : -1;
+    const long long pix = valid ? (spare ? P : (long long)q.rec.r.pad) : -1;
+    const long long kin = valid && !spare && q.rec.r.pad2 >= 0 && q.rec.r.pad2 < P
+                              ? (long long)q.rec.r.pad2 : -1;
     long long prev = __shfl_up(pix, 1, 64);
     if (lane == 0) prev = pd;
     const long long kw = kin >= 0 ? kin : pw;
@@ -2747,7 +2833,6 @@ __global__ void __launch_bounds__(256) k_shard_unpack(
     if (valid) {
       const int idx = idx0 + i;
       deprec[pix] = q.rec;
-      wcarry[pix] = q.pcol;
       dep_pix[idx] = pix;
       if (st) {
         const int s = s0 + __popcll(ms & lt);
@@ -2765,11 +2850,14 @@ __global__ void __launch_bounds__(256) k_shard_unpack(
 
 // Root: image row y <- gathered[y % G][y / G] (the row-cyclic partition undone).
 __global__ void __launch_bounds__(256) k_deinterleave(const uint8_t* __restrict__ gathered,
+                                                      const uint8_t* __restrict__ block0,
                                                       int G, int rmax, int W, int H,
                                                       uint8_t* __restrict__ img) {
   const int y = blockIdx.x;
   const size_t rb = (size_t)W * 3;
-  const uint8_t* src = gathered + ((size_t)(y % G) * rmax + y / G) * rb;
+  // rank 0's rows come from the root's own block (not copied into `gathered`)
+  const uint8_t* src = (y % G == 0 && block0) ? block0 + (size_t)(y / G) * rb
+                                              : gathered + ((size_t)(y % G) * rmax + y / G) * rb;
   uint8_t* dst = img + (size_t)y * rb;
   if ((rb & 3) == 0) {
     for (size_t i = threadIdx.x; i < rb / 4; i += blockDim.x)
@@ -2837,10 +2925,10 @@ hipError_t launch_parity(const LaunchScene& s, int W, int H, int maxrec, uint8_t
   dim3 grid((W + kTileW - 1) / kTileW, (H + kTileH - 1) / kTileH);
   if (w.side && w.split_shade)   // carry part only; colours shaded beside the resolver (k_side)
     hipLaunchKernelGGL(st ? k_classify<true> : k_classify<false>, grid, dim3(kBlock), 0, stream, sc, cam, W, H, maxrec, w.cls,
-                       w.wcarry, (DepRec*)w.deprec);
+                       w.wcarry, (DepLine*)w.deprec);
   else
     hipLaunchKernelGGL(st ? k_phase_a<true> : k_phase_a<false>, grid, dim3(kBlock), 0, stream, sc, cam, W, 0, 1, H, maxrec, out,
-                       w.cls, w.wcarry, (DepRec*)w.deprec, zcount);
+                       w.cls, w.wcarry, (DepLine*)w.deprec, zcount);
   if (ev) (void)hipEventRecord(ev[0], stream);
   if (w.adone) (void)hipEventRecord(w.adone, stream);
   // frames in flight: the compaction (small latency-bound kernels that gate this frame's
@@ -2877,7 +2965,7 @@ hipError_t launch_parity(const LaunchScene& s, int W, int H, int maxrec, uint8_t
   }
   auto kres = s.n <= kLdsShapes ? k_resolve<true> : k_resolve<false>;
   hipLaunchKernelGGL(kres, dim3(w.resolve_blocks), dim3(kResolveBlock), w.resolve_lds, rs, sc,
-                     maxrec, (const DepRec*)w.deprec, w.dep_pix, w.seg_key, w.wcarry,
+                     maxrec, (const DepLine*)w.deprec, w.dep_pix, w.seg_key, w.wcarry,
                      w.seg_start, w.seg_order, w.counters, w.counters + 1, (CinG*)w.cin, w.team_blocks,
                      w.long_len, (TeamState*)w.team, w.trace, w.coop_group, w.wave_k,
                      w.resolve_k, w.resolve_clean > 0 ? w.resolve_clean : 1, w.team_cscan, w.epoch, w.helpers, w.hand_run, w.inject, w.block_min,
@@ -2893,7 +2981,7 @@ hipError_t launch_parity(const LaunchScene& s, int W, int H, int maxrec, uint8_t
   if (w.side) {   // colours and phase C beside the resolver
     (void)hipStreamWaitEvent(w.side, w.fork, 0);
     hipLaunchKernelGGL(st ? k_side<true> : k_side<false>, dim3(w.side_blocks), dim3(kSideBlock), w.side_lds, w.side, sc, cam,
-                       W, H, maxrec, w.cls, w.dep_pix, (const DepRec*)w.deprec, w.wcarry,
+                       W, H, maxrec, w.cls, w.dep_pix, (const DepLine*)w.deprec,
                        (CinG*)w.cin, w.counters,
                        w.batch_state, w.batch_rq,
                        out, w.patch, zcount, (TeamState*)w.team, w.resolve_blocks, w.epoch,
@@ -2920,7 +3008,7 @@ static void enqueue_phase_c(const Scene& sc, const Cam& cam, bool st, int W, int
                             hipStream_t stream) {
   if (w.side || w.inres || w.phase_c_finish) {   // what k_side / the resolver's waves left
     hipLaunchKernelGGL(st ? k_finish<true> : k_finish<false>, dim3(w.phase_c_blocks), dim3(kBlock), 0, stream, sc, cam, W, H,
-                       maxrec, w.cls, w.dep_pix, (const DepRec*)w.deprec, w.wcarry,
+                       maxrec, w.cls, w.dep_pix, (const DepLine*)w.deprec,
                        (CinG*)w.cin, w.counters, w.batch_state,
                        out, w.patch,
                        zcount, (TeamState*)w.team, w.epoch, (w.side && w.split_shade) ? 1 : 0,
@@ -2929,7 +3017,7 @@ static void enqueue_phase_c(const Scene& sc, const Cam& cam, bool st, int W, int
     hipLaunchKernelGGL((sc.dep_fast ? (st ? k_dep_chunks<true, true> : k_dep_chunks<false, true>)
                                : (st ? k_dep_chunks<true, false> : k_dep_chunks<false, false>)), dim3(w.phase_c_blocks),
                        dim3(kBlock), 0, stream, sc, cam, W, 0, 1, maxrec, w.dep_pix,
-                       (const DepRec*)w.deprec, (const float4*)w.wcarry, (CinG*)w.cin,
+                       (const DepLine*)w.deprec, (CinG*)w.cin,
                        w.counters, out, w.patch, zcount, (TeamState*)w.team, w.epoch,
                        0x7fffffff);
   }
@@ -3025,7 +3113,7 @@ hipError_t launch_shard_local(const LaunchScene& s, int W, int H, int row0, int 
   dim3 grid((W + kTileW - 1) / kTileW, (nrows + kTileH - 1) / kTileH);
   hipLaunchKernelGGL(st ? k_phase_a<true> : k_phase_a<false>, grid, dim3(kBlock), 0, stream, sc,
                      cam, W, row0, row_step, nrows, maxrec, out, w.cls, w.wcarry,
-                     (DepRec*)w.deprec, zcount);
+                     (DepLine*)w.deprec, zcount);
   const int row_blocks = (nrows + kRowWaves - 1) / kRowWaves;
   hipLaunchKernelGGL(k_row_stats, dim3(row_blocks), dim3(256), 0, stream, w.cls, W, nrows,
                      (RowStats*)w.row_stats, nullptr, nullptr, 0, nullptr, 0);
@@ -3033,13 +3121,13 @@ hipError_t launch_shard_local(const LaunchScene& s, int W, int H, int row0, int 
                      (const RowStats*)w.row_stats, w.row_off, w.row_soff, w.row_prevw,
                      w.row_prevd, w.counters);
   hipLaunchKernelGGL(k_shard_pack, dim3(row_blocks), dim3(256), 0, stream, w.cls, w.wcarry,
-                     (const DepRec*)w.deprec, W, row0, row_step, nrows, w.row_off, w.dep_pix,
+                     (const DepLine*)w.deprec, W, row0, row_step, nrows, w.row_off, w.dep_pix,
                      (ShardEntry*)ent, (RowShard*)rows);
   return hipGetLastError();
 }
 
 hipError_t launch_shard_resolve(const LaunchScene& s, int W, int H, int G, int rmax,
-                                const void* rows_all, const void* ent_all,
+                                const void* rows_all, const void* ent_all, const void* ent0,
                                 const long long* offs, int maxrec, const ParityWork& w,
                                 uint8_t* out, unsigned long long* zcount, hipStream_t stream,
                                 const hipEvent_t* ev, int bound) {
@@ -3057,8 +3145,9 @@ hipError_t launch_shard_resolve(const LaunchScene& s, int W, int H, int G, int r
                      w.row_off, w.row_soff, w.row_prevw, w.row_prevd, w.counters);
   const int row_blocks = (H + kRowWaves - 1) / kRowWaves;
   hipLaunchKernelGGL(k_shard_unpack, dim3(row_blocks), dim3(256), 0, stream, rs,
-                     (const ShardEntry*)ent_all, o, G, rmax, W, H, w.row_off, w.row_soff,
-                     w.row_prevw, w.row_prevd, (DepRec*)w.deprec, w.dep_pix, w.seg_start,
+                     (const ShardEntry*)ent_all, (const ShardEntry*)ent0, o, G, rmax, W, H,
+                     w.row_off, w.row_soff,
+                     w.row_prevw, w.row_prevd, (DepLine*)w.deprec, w.dep_pix, w.seg_start,
                      w.seg_key, w.wcarry, bound);
   hipLaunchKernelGGL(k_seg_order, dim3(1), dim3(1024), 0, stream, w.seg_start, w.counters,
                      w.seg_order, w.batch_state, w.batch_cnt, w.batch_rq, w.block_min,
@@ -3069,7 +3158,7 @@ hipError_t launch_shard_resolve(const LaunchScene& s, int W, int H, int G, int r
   // already hold — and k_finish takes what its waves left
   auto kres = s.n <= kLdsShapes ? k_resolve<true> : k_resolve<false>;
   hipLaunchKernelGGL(kres, dim3(w.resolve_blocks), dim3(kResolveBlock), w.resolve_lds, stream,
-                     sc, maxrec, (const DepRec*)w.deprec, w.dep_pix, w.seg_key, w.wcarry,
+                     sc, maxrec, (const DepLine*)w.deprec, w.dep_pix, w.seg_key, w.wcarry,
                      w.seg_start, w.seg_order, w.counters, w.counters + 1, (CinG*)w.cin,
                      w.team_blocks, w.long_len, (TeamState*)w.team, w.trace, w.coop_group,
                      w.wave_k, w.resolve_k, w.resolve_clean > 0 ? w.resolve_clean : 1,
@@ -3081,14 +3170,15 @@ hipError_t launch_shard_resolve(const LaunchScene& s, int W, int H, int G, int r
   return hipGetLastError();
 }
 
-hipError_t launch_deinterleave(const uint8_t* gathered, int G, int rmax, int W, int H,
-                               uint8_t* img, hipStream_t stream) {
+hipError_t launch_deinterleave(const uint8_t* gathered, const uint8_t* block0, int G, int rmax,
+                               int W, int H, uint8_t* img, hipStream_t stream) {
   if (H <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_deinterleave, dim3(H), dim3(256), 0, stream, gathered, G, rmax, W, H, img);
+  hipLaunchKernelGGL(k_deinterleave, dim3(H), dim3(256), 0, stream, gathered, block0, G, rmax, W,
+                     H, img);
   return hipGetLastError();
 }
 
-size_t deprec_bytes() { return sizeof(DepRec); }
+size_t deprec_bytes() { return sizeof(DepLine); }   // one line per pixel (DepLine)
 size_t row_stats_bytes() { return sizeof(RowStats); }
 
 }  // namespace rc

@@ -67,7 +67,8 @@ struct FrameLog {
     int rq_prod, rq_cons, helpers_out;
     int n_scan, n_cscan, n_resolve; // the frame's team rounds by kind
     int spin_ticks[4];              // its longest bounded waits per spin site (10 ns ticks)
-    int pad[2];
+    int clock_mhz;                  // shader clock over its resolver's run (0: not measured)
+    int pad;
   };
   // Frame diagnostics of the entries read back since the last diag_take(): frames, the most
   // team rounds of each kind in one frame, the longest wait per spin site.
@@ -75,6 +76,7 @@ struct FrameLog {
     long long frames = 0;
     int scan_max = 0, cscan_max = 0, resolve_max = 0;
     int spin_ticks_max[4] = {0, 0, 0, 0};
+    int clock_min = 0, clock_max = 0;   // MHz, over the frames that measured it
   };
   Diag diag;
   Entry* ring = nullptr;     // pinned host memory, kRing entries

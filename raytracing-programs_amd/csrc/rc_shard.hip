@@ -184,9 +184,11 @@ int gather_fixed(rc_group& g, const std::vector<const void*>& send, void* recv, 
 }
 
 // root.recv[off[r] ..] <- rank r's send (bytes[r] bytes; the root knows every rank's size, a
-// rank its own)
+// rank its own).  self = false: the root's own part stays where it is (the reader takes it in
+// place), so nothing is copied for rank 0 — at G = 1 nothing moves at all.
 int gather_var(rc_group& g, const std::vector<const void*>& send, void* recv,
-               const std::vector<size_t>& off, const std::vector<size_t>& bytes) {
+               const std::vector<size_t>& off, const std::vector<size_t>& bytes,
+               bool self = true) {
   if (g.transport == RC_XFER_RCCL) {
     NCCL_TRY(ncclGroupStart());
     for (size_t i = 0; i < g.ranks.size(); ++i) {
@@ -200,7 +202,7 @@ int gather_var(rc_group& g, const std::vector<const void*>& send, void* recv,
           NCCL_TRY(ncclRecv((char*)recv + off[q], bytes[q], ncclUint8, q, r.comm, r.stream));
     }
     NCCL_TRY(ncclGroupEnd());
-    if (g.root && bytes[0]) {   // the root's own part
+    if (self && g.root && bytes[0]) {   // the root's own part
       HIP_TRY(hipSetDevice(g.root->device));
       HIP_TRY(hipMemcpyAsync(recv, send[0], bytes[0], hipMemcpyDeviceToDevice, g.root->stream));
     }
@@ -216,7 +218,7 @@ int gather_var(rc_group& g, const std::vector<const void*>& send, void* recv,
   for (size_t i = 0; i < g.ranks.size(); ++i) {
     Rank& r = *g.ranks[i];
     if (&r != &root) HIP_TRY(hipStreamWaitEvent(root.stream, r.ready, 0));
-    if (bytes[r.rank])
+    if (bytes[r.rank] && (self || &r != &root))
       HIP_TRY(hipMemcpyAsync((char*)recv + off[r.rank], send[i], bytes[r.rank], hipMemcpyDefault,
                              root.stream));
   }
@@ -423,12 +425,11 @@ int render_sharded(rc_group& g, const rc_scene* s, int W, int H, const rc_option
         return -1;
       }
     }
-    // 3. the entries to the root
+    // 3. the other ranks' entries to the root (its own are read in place); the same point-to-
+    //    point pattern for the fixed-size and the exact exchange, only the sizes differ
     std::vector<const void*> se;
     for (auto& rp : g.ranks) se.push_back(rp->ent.p);
-    if (fixed ? gather_fixed(g, se, root ? root->ent_all.p : nullptr, eb[0])
-              : gather_var(g, se, root ? root->ent_all.p : nullptr, eo, eb))
-      return -1;
+    if (gather_var(g, se, root ? root->ent_all.p : nullptr, eo, eb, false)) return -1;
   }
   // 4. the row blocks and the phase-A / render event counts to the root, the interleave undone
   //    there (parity: into the root's image, ahead of the resolver; its DEP pixels follow)
@@ -440,16 +441,21 @@ int render_sharded(rc_group& g, const rc_scene* s, int W, int H, const rc_option
     sf.push_back(rp->frame.p);
     sz.push_back(rp->small.p);
   }
-  if (gather_fixed(g, sf, root ? root->frames_all.p : nullptr, block_bytes) ||
-      gather_fixed(g, sz, root ? root->small_all.p : nullptr, 16))
-    return -1;
+  {   // the other ranks' blocks (the root de-interleaves its own in place)
+    std::vector<size_t> fo(G), fb(G, block_bytes);
+    for (int q = 0; q < G; ++q) fo[q] = (size_t)q * block_bytes;
+    if (gather_var(g, sf, root ? root->frames_all.p : nullptr, fo, fb, false) ||
+        gather_fixed(g, sz, root ? root->small_all.p : nullptr, 16))
+      return -1;
+  }
   for (auto& rp : g.ranks) {
     HIP_TRY(hipSetDevice(rp->device));
     HIP_TRY(hipEventRecord(rp->rev[2], rp->stream));
   }
   if (root) {
     HIP_TRY(hipSetDevice(root->device));
-    HIP_TRY(rc::launch_deinterleave((const uint8_t*)root->frames_all.p, G, rmax, W, H,
+    HIP_TRY(rc::launch_deinterleave((const uint8_t*)root->frames_all.p,
+                                    (const uint8_t*)root->frame.p, G, rmax, W, H,
                                     parity ? img : d_image, root->stream));
   }
   // 5. parity, the root: the resolver with phase C inside it, into the root's image
@@ -481,7 +487,8 @@ int render_sharded(rc_group& g, const rc_scene* s, int W, int H, const rc_option
       HIP_TRY(hipMemsetAsync(rz, 0, sizeof(unsigned long long), root->stream));
       hipEvent_t rev[2] = {root->ev[2], root->ev[3]};
       HIP_TRY(rc::launch_shard_resolve(ls[0], W, H, G, rmax, root->rows_all.p, root->ent_all.p,
-                                       offs.data(), maxrec, wr, img, rz, root->stream, rev,
+                                       root->ent.p, offs.data(), maxrec, wr, img, rz,
+                                       root->stream, rev,
                                        fixed ? (int)per_rank : 0x7fffffff));
       HIP_TRY(hipEventRecord(root->ev[4], root->stream));
       if (d_image != img)

@@ -693,3 +693,39 @@ def test_render_device_two_streams(scenes, table):
         want = table[f"{name}:{n}x{n}:d{d}:parity"]["md5"]
         assert res[i] == [want] * 3, name
     assert rc.lone_frames_check()["failed"] == 0
+
+
+def test_resolver_diagnostics_record(scenes, table):
+    """a frame's own record explains a slow frame.  After frames in flight
+    and lone frames, rc_resolver_stats_get reports every frame read back, the resolver's
+    placement within what a CU can hold (registers <= 256: two lane workgroups per CU), the
+    team's rounds, and the shader clock each resolver ran at (s_memtime against s_memrealtime:
+    a throttled box would show a low clock, not an unexplained slow step)."""
+    torch = pytest.importorskip("torch")
+    n, key = 1024, "quadric:1024x1024:d6:parity"
+    want = table[key]["md5"]
+    s = scenes["quadric"]
+    bufs = [torch.zeros((n, n, 3), dtype=torch.uint8, device="cuda") for _ in range(4)]
+    torch.cuda.synchronize()
+    rc.frames_wait()
+    for b in bufs:
+        rc.frame_submit(s, n, n, b.data_ptr(), depth=6)
+    rc.frames_wait()
+    d = rc.resolver_stats()
+    assert d["frames"] == 4
+    assert 0 < d["resolve_ms_min"] <= d["resolve_ms_mean"] <= d["resolve_ms_max"]
+    assert 0 < d["wg_per_cu"] <= d["wg_per_cu_max"] and d["regs"] <= 256
+    assert 300 <= d["clock_mhz_min"] <= d["clock_mhz_max"] <= 3500, d
+    assert d["scan_rounds_max"] + d["cscan_rounds_max"] + d["resolve_rounds_max"] > 0
+    for b in bufs:
+        assert p3_md5(b.cpu().numpy()) == want
+    rc.lone_frames_check()
+    rc.resolver_stats(lone=True)   # reset the lone window
+    out = torch.empty((n, n, 3), dtype=torch.uint8, device="cuda")
+    for _ in range(3):
+        rc.render_device(s, n, n, out.data_ptr(), depth=6)
+    assert rc.lone_frames_check() == {"checked": 3, "failed": 0}
+    d = rc.resolver_stats(lone=True)
+    assert d["frames"] == 3 and 300 <= d["clock_mhz_min"] <= d["clock_mhz_max"] <= 3500, d
+    assert d["wg_per_cu"] <= d["wg_per_cu_max"]
+    assert p3_md5(out.cpu().numpy()) == want
