@@ -42,8 +42,8 @@ rc_tuning default_tuning() {
   t.resolve_lds_kb = 0;
   t.resolve_grid = 0;
   t.team_blocks = -1;
-  t.helpers = 8;
-  t.hand_run = 512;
+  t.helpers = 16;    // round 4: 8 -> 16 with hand_run 512 -> 128 (lone quadric 4096^2 5.01 ->
+  t.hand_run = 128;  // 4.65-4.77 ms, 8192^2 13.1 -> 12.3 ms; profiles/r04j_helpers_*.txt)
   t.long_len = 32768;
   t.wave_k = 2;
   t.resolve_k = 1;

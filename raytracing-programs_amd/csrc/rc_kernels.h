@@ -104,10 +104,13 @@ size_t shard_entry_bytes();   // one DEP entry on the wire
 size_t shard_row_bytes();     // one row summary on the wire
 // A rank: phase A on rows row0 + k*row_step (k < nrows) into rank-local buffers, the local
 // DEP list (w.dep_pix, local pixels; w.counters[2] = entries) and the wire entries / rows.
+// img_rec / img_wcarry (the root): DEP lines and writer carries go straight to the root
+// resolver's image-indexed buffers and its entries are thin {image pixel, writer} pairs.
 hipError_t launch_shard_local(const LaunchScene& s, int W, int H, int row0, int row_step,
                               int nrows, int maxrec, uint8_t* out, const ParityWork& w,
                               void* ent, void* rows, unsigned long long* zcount,
-                              hipStream_t stream);
+                              hipStream_t stream, void* img_rec = nullptr,
+                              float4* img_wcarry = nullptr);
 // The root: image scan order from the gathered rows ([G][rmax]) and entries (rank g's at
 // offs[g]) in a lone frame's layout (pixel-indexed records, primary shades and writer carries
 // in w.deprec / w.wcarry, which hold W*H + 1 pixels: the last is a spare for entries beyond a
@@ -120,7 +123,7 @@ hipError_t launch_shard_resolve(const LaunchScene& s, int W, int H, int G, int r
                                 const void* rows_all, const void* ent_all, const void* ent0,
                                 const long long* offs, int maxrec, const ParityWork& w,
                                 uint8_t* out, unsigned long long* zcount, hipStream_t stream,
-                                const hipEvent_t* ev, int bound = 0x7fffffff);
+                                const hipEvent_t* ev, int bound = 0x7fffffff, int thin0 = 0);
 // The root: image <- gathered row blocks [G][rmax][W*3]; block0 (optional): rank 0's block in
 // place of gathered[0] (the root's own rows are not copied).
 hipError_t launch_deinterleave(const uint8_t* gathered, const uint8_t* block0, int G, int rmax,

@@ -71,22 +71,28 @@ static_assert(kTileW % 8 == 0 && kTileH % 8 == 0, "8x8 wave tiles");
 // each with its own L2).  With the grid's own order, horizontally adjacent tiles run on
 // different XCDs, so a 128-byte line of class bytes (8 tiles wide) or of framebuffer bytes
 // (~3 tiles) is written piecewise from several L2s and reaches HBM as partial-line writes
-// (rocprofv3 WRITE_SIZE of k_phase_a 1.26x its bytes).  Here XCD k takes the k-th contiguous
-// range of tiles in row-major order, so a line's tiles share one L2 and merge there.
+// (rocprofv3 WRITE_SIZE of k_phase_a 1.26x its bytes).
+//   RC_XCD_TILES 1: XCD k takes the k-th contiguous eighth of the tiles — measured: phase A
+//                   0.745 -> 0.878 ms (the image's heavy bands land on a few XCDs);
+//   RC_XCD_TILES 2: chunks of 8 horizontally adjacent tiles per XCD, chunks dealt round-robin
+//                   (a line's tiles share one L2; the load stays interleaved).
 #ifndef RC_XCD_TILES
-#define RC_XCD_TILES 1
+#define RC_XCD_TILES 2   // measured: k_phase_a WRITE_SIZE 312 -> 269 MB in flight, time within noise
 #endif
 __device__ __forceinline__ void xcd_tile(int& bx, int& by) {
-  if (!RC_XCD_TILES) {
-    bx = blockIdx.x;
-    by = blockIdx.y;
-    return;
-  }
   const int nx = gridDim.x, n = nx * (int)gridDim.y;
   const int lin = (int)blockIdx.y * nx + (int)blockIdx.x;
-  const int xcd = lin & 7, k = lin >> 3, q = n >> 3, r = n & 7;
-  // XCDs below r take q + 1 tiles, the others q: a bijection of [0, n)
-  const int t = xcd < r ? xcd * (q + 1) + k : r * (q + 1) + (xcd - r) * q + k;
+  int t = lin;
+  if (RC_XCD_TILES == 1) {
+    const int xcd = lin & 7, k = lin >> 3, q = n >> 3, r = n & 7;
+    // XCDs below r take q + 1 tiles, the others q: a bijection of [0, n)
+    t = xcd < r ? xcd * (q + 1) + k : r * (q + 1) + (xcd - r) * q + k;
+  } else if (RC_XCD_TILES == 2 && lin < (n & ~63)) {
+    // the XCD's k-th workgroup -> chunk (k / 8) * 8 + xcd, tile k % 8 of it (a bijection of
+    // the first n & ~63 tiles; the rest keep the grid order)
+    const int xcd = lin & 7, k = lin >> 3;
+    t = ((k >> 3) * 8 + xcd) * 8 + (k & 7);
+  }
   bx = t % nx;
   by = t / nx;
 }
@@ -300,7 +306,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_
                                                     uint8_t* __restrict__ cls,
                                                     float4* __restrict__ wcarry,
                                                     DepLine* __restrict__ deprec,
-                                                    unsigned long long* __restrict__ zcount) {
+                                                    unsigned long long* __restrict__ zcount,
+                                                    int rpitch) {
   if (!RC_X0_PIXEL) sc.has_quadric = sc.has_quadric != 0;   // no cross-term-free form here (RC_X0_*)
   __shared__ StageBuf<kStage> stage;
   __shared__ TileBytes tb;
@@ -324,14 +331,18 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_
     shoot<kModeParityA>(sc, d, maxrec, v3(0.0f, 0.0f, 0.0f), po, zero);
     if (RC_TILE_STAGE) ((uint8_t*)tb.cls[ly])[lx] = po.cls;
     else cls[p] = po.cls;
+    // DEP lines and writer carries at row pitch rpitch (W: the local pixel; a row shard's root
+    // passes G * W with the buffers offset by row0 * W: the IMAGE pixel, i.e. straight into the
+    // root resolver's lone-frame layout, k_shard_pack thin entries)
+    const size_t pr = (size_t)y * rpitch + x;
     if (po.cls == kClsDep) {
       // one 64-byte line: the record and, under dep_fast, the primary shade for phase C; this
       // part's events are counted here (else phase C recomputes the whole pixel and counts its
       // events).  The pixel's framebuffer bytes are phase C's: the tile writes a placeholder.
       if (!RC_EXP_NODEPW) {
-        deprec[p].r = po.dep;
+        deprec[pr].r = po.dep;
         if (sc.dep_fast)
-          *(float4*)&deprec[p].px = make_float4(po.pcol.x, po.pcol.y, po.pcol.z, 0.0f);
+          *(float4*)&deprec[pr].px = make_float4(po.pcol.x, po.pcol.y, po.pcol.z, 0.0f);
       }
       if (sc.dep_fast) flush_events(zero, zcount);
       if (RC_TILE_STAGE) tile_put_rgb(tb, lx, ly, 0, 0, 0, nullptr);
@@ -342,7 +353,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_
     const unsigned long long mw = __ballot(po.cls == kClsWriter);
     const unsigned long long md = __ballot(po.cls == kClsDep);
     if (po.cls == kClsWriter && writer_may_key(mw, md))
-      wcarry[p] = make_float4(po.carry.x, po.carry.y, po.carry.z, 0.0f);
+      wcarry[pr] = make_float4(po.carry.x, po.carry.y, po.carry.z, 0.0f);
   }
   if (!tile_last_wave(tb)) return;
   const int nx = W - x0 < kTileW ? W - x0 : kTileW;
@@ -2706,12 +2717,15 @@ __global__ void __launch_bounds__(256) k_shard_pack(
     const uint8_t* __restrict__ cls, const float4* __restrict__ wcarry,
     const DepLine* __restrict__ deprec, int W, int row0, int row_step, int nrows,
     const int* __restrict__ row_off, long long* __restrict__ dep_pix,
-    ShardEntry* __restrict__ ent, RowShard* __restrict__ rs) {
+    ShardEntry* __restrict__ ent, RowShard* __restrict__ rs, int thin) {
   const int y = blockIdx.x * kRowWaves + (int)(threadIdx.x >> 6);
   if (y >= nrows) return;
   const int lane = threadIdx.x & 63;
   const long long lbase = (long long)y * W;
   const long long gbase = (long long)(row0 + (long long)y * row_step) * W;
+  // thin (the root): records and writer carries are already at their image pixels (k_phase_a
+  // rec_img); an entry is only {image pixel, in-row writer before it} (8 B, read in place)
+  const long long wbase = thin ? gbase : lbase;
   const unsigned long long lt = lanemask_lt();
   int l0 = row_off[y], nd = 0, ns = 0;
   int lw = -1, ld = -1, wf = -1;   // x of the row's last writer / last DEP / first DEP's writer
@@ -2733,12 +2747,16 @@ __global__ void __launch_bounds__(256) k_shard_pack(
     if (dep) {
       const int l = l0 + __popcll(md & lt);
       dep_pix[l] = lbase + x;
-      ShardEntry e;
-      e.rec = deprec[lbase + x];
-      e.rec.r.pad = (int)(gbase + x);
-      e.rec.r.pad2 = kw >= 0 ? (int)(gbase + kw) : -1;
-      e.kc = kw >= 0 ? wcarry[lbase + kw] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-      ent[l] = e;
+      if (thin) {
+        ((int2*)ent)[l] = make_int2((int)(gbase + x), kw >= 0 ? (int)(gbase + kw) : -1);
+      } else {
+        ShardEntry e;
+        e.rec = deprec[lbase + x];
+        e.rec.r.pad = (int)(gbase + x);
+        e.rec.r.pad2 = kw >= 0 ? (int)(gbase + kw) : -1;
+        e.kc = kw >= 0 ? wcarry[lbase + kw] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        ent[l] = e;
+      }
     }
     l0 += __popcll(md);
     nd += __popcll(md);
@@ -2754,7 +2772,7 @@ __global__ void __launch_bounds__(256) k_shard_pack(
     r.lastw = lw >= 0 ? gbase + lw : -1;
     r.lastd = ld >= 0 ? gbase + ld : -1;
     r.wfirst = wf >= 0 ? gbase + wf : -1;
-    r.cw = lw >= 0 ? wcarry[lbase + lw] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    r.cw = lw >= 0 ? wcarry[wbase + lw] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     rs[y] = r;
   }
 }
@@ -2786,15 +2804,19 @@ __global__ void __launch_bounds__(256) k_shard_unpack(
     const int* __restrict__ row_soff, const long long* __restrict__ row_prevw,
     const long long* __restrict__ row_prevd, DepLine* __restrict__ deprec,
     long long* __restrict__ dep_pix, int* __restrict__ seg_start,
-    long long* __restrict__ seg_key, float4* __restrict__ wcarry, int bound) {
+    long long* __restrict__ seg_key, float4* __restrict__ wcarry, int bound, int thin0) {
   const int y = blockIdx.x * kRowWaves + (int)(threadIdx.x >> 6);
   if (y >= H) return;
   const int lane = threadIdx.x & 63;
   const long long P = (long long)W * H;
   const int g = y % G;
   const RowShard r = rsall[(size_t)g * rmax + y / G];
-  // rank 0's entries are the root's own list (never copied), the others' the gathered blocks
+  // rank 0's entries are the root's own list (never copied), the others' the gathered blocks;
+  // thin0: the root's list is {image pixel, writer} pairs whose records and writer carries its
+  // phase A already wrote at their image pixels (k_shard_pack thin)
+  const bool th = g == 0 && ent0 && thin0;
   const ShardEntry* e = (g == 0 && ent0 ? ent0 : ent + offs.off[g]) + r.loff;
+  const int2* et = (const int2*)ent0 + r.loff;
   const int n = r.ndep;
   const int idx0 = row_off[y];
   int s0 = row_soff[y];
@@ -2810,13 +2832,19 @@ __global__ void __launch_bounds__(256) k_shard_unpack(
     const int i = i0 + lane;
     const bool valid = i < n;
     ShardEntry q;
-    if (valid) q = e[i];
+    if (valid && !th) q = e[i];
+    if (valid && th) {
+      const int2 tq = et[i];
+      q.rec.r.pad = tq.x;
+      q.rec.r.pad2 = tq.y;
+    }
     // bound: the fixed-size exchange delivered each rank's first `bound` entries.  A longer
     // list (the frame is then rendered again, rc_shard.hip) reads the next rank's block: such
     // an entry becomes a harmless record (zero directions, shape 0) at the spare pixel P (the
     // root's buffers hold P + 1 pixels), continuing its segment — never an out-of-range shape
-    // or pixel index for the resolver and phase C
-    const bool spare = valid && (r.loff + i >= bound || q.rec.r.pad < 0 || q.rec.r.pad >= P);
+    // or pixel index for the resolver and phase C.  The root's own list is read in place: whole.
+    const bool spare = valid && ((!th && r.loff + i >= bound) || q.rec.r.pad < 0 ||
+                                 q.rec.r.pad >= P);
     if (spare) {
       q.rec = DepLine{DepRec{0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0, -1, 0.0f, 0.0f, 0.0f, -1},
                       0.0f, 0.0f, 0.0f, 0};
@@ -2832,14 +2860,15 @@ __global__ void __launch_bounds__(256) k_shard_unpack(
     const unsigned long long ms = __ballot(st);
     if (valid) {
       const int idx = idx0 + i;
-      deprec[pix] = q.rec;
+      if (!th || spare) deprec[pix] = q.rec;
       dep_pix[idx] = pix;
       if (st) {
         const int s = s0 + __popcll(ms & lt);
         seg_start[s] = idx;
         seg_key[s] = kw;
-        if (kw >= 0) wcarry[kw] = kin >= 0 ? q.kc : pwc;   // every entry keyed by kw writes
-                                                           // the same carry-out
+        // every entry keyed by kw writes the same carry-out; the root's own in-row writers'
+        // carries are in place already
+        if (kw >= 0 && !(th && kin >= 0)) wcarry[kw] = kin >= 0 ? q.kc : pwc;
       }
     }
     s0 += __popcll(ms);
@@ -2928,7 +2957,7 @@ hipError_t launch_parity(const LaunchScene& s, int W, int H, int maxrec, uint8_t
                        w.wcarry, (DepLine*)w.deprec);
   else
     hipLaunchKernelGGL(st ? k_phase_a<true> : k_phase_a<false>, grid, dim3(kBlock), 0, stream, sc, cam, W, 0, 1, H, maxrec, out,
-                       w.cls, w.wcarry, (DepLine*)w.deprec, zcount);
+                       w.cls, w.wcarry, (DepLine*)w.deprec, zcount, W);
   if (ev) (void)hipEventRecord(ev[0], stream);
   if (w.adone) (void)hipEventRecord(w.adone, stream);
   // frames in flight: the compaction (small latency-bound kernels that gate this frame's
@@ -3103,8 +3132,9 @@ size_t shard_row_bytes() { return sizeof(RowShard); }
 hipError_t launch_shard_local(const LaunchScene& s, int W, int H, int row0, int row_step,
                               int nrows, int maxrec, uint8_t* out, const ParityWork& w,
                               void* ent, void* rows, unsigned long long* zcount,
-                              hipStream_t stream) {
+                              hipStream_t stream, void* img_rec, float4* img_wcarry) {
   const Scene sc = make_scene(s);
+  const bool thin = img_rec && img_wcarry;
   const Cam cam = make_cam(s, W, H);
   const bool st = stage_fits(s);
   (void)hipMemsetAsync(w.counters, 0, 16 * sizeof(int), stream);
@@ -3112,17 +3142,19 @@ hipError_t launch_shard_local(const LaunchScene& s, int W, int H, int row0, int 
   if (nrows <= 0) return hipGetLastError();
   dim3 grid((W + kTileW - 1) / kTileW, (nrows + kTileH - 1) / kTileH);
   hipLaunchKernelGGL(st ? k_phase_a<true> : k_phase_a<false>, grid, dim3(kBlock), 0, stream, sc,
-                     cam, W, row0, row_step, nrows, maxrec, out, w.cls, w.wcarry,
-                     (DepLine*)w.deprec, zcount);
+                     cam, W, row0, row_step, nrows, maxrec, out, w.cls,
+                     thin ? img_wcarry + (size_t)row0 * W : w.wcarry,
+                     thin ? (DepLine*)img_rec + (size_t)row0 * W : (DepLine*)w.deprec, zcount,
+                     thin ? row_step * W : W);
   const int row_blocks = (nrows + kRowWaves - 1) / kRowWaves;
   hipLaunchKernelGGL(k_row_stats, dim3(row_blocks), dim3(256), 0, stream, w.cls, W, nrows,
                      (RowStats*)w.row_stats, nullptr, nullptr, 0, nullptr, 0);
   hipLaunchKernelGGL(k_row_scan, dim3(1), dim3(1024), 0, stream, nrows,
                      (const RowStats*)w.row_stats, w.row_off, w.row_soff, w.row_prevw,
                      w.row_prevd, w.counters);
-  hipLaunchKernelGGL(k_shard_pack, dim3(row_blocks), dim3(256), 0, stream, w.cls, w.wcarry,
-                     (const DepLine*)w.deprec, W, row0, row_step, nrows, w.row_off, w.dep_pix,
-                     (ShardEntry*)ent, (RowShard*)rows);
+  hipLaunchKernelGGL(k_shard_pack, dim3(row_blocks), dim3(256), 0, stream, w.cls,
+                     thin ? img_wcarry : w.wcarry, (const DepLine*)w.deprec, W, row0, row_step,
+                     nrows, w.row_off, w.dep_pix, (ShardEntry*)ent, (RowShard*)rows, thin ? 1 : 0);
   return hipGetLastError();
 }
 
@@ -3130,7 +3162,7 @@ hipError_t launch_shard_resolve(const LaunchScene& s, int W, int H, int G, int r
                                 const void* rows_all, const void* ent_all, const void* ent0,
                                 const long long* offs, int maxrec, const ParityWork& w,
                                 uint8_t* out, unsigned long long* zcount, hipStream_t stream,
-                                const hipEvent_t* ev, int bound) {
+                                const hipEvent_t* ev, int bound, int thin0) {
   if (G < 1 || G > kMaxShards || w.side || w.patch) return hipErrorInvalidValue;
   const Scene sc = make_scene(s);
   const Cam cam = make_cam(s, W, H);
@@ -3148,7 +3180,7 @@ hipError_t launch_shard_resolve(const LaunchScene& s, int W, int H, int G, int r
                      (const ShardEntry*)ent_all, (const ShardEntry*)ent0, o, G, rmax, W, H,
                      w.row_off, w.row_soff,
                      w.row_prevw, w.row_prevd, (DepLine*)w.deprec, w.dep_pix, w.seg_start,
-                     w.seg_key, w.wcarry, bound);
+                     w.seg_key, w.wcarry, bound, thin0);
   hipLaunchKernelGGL(k_seg_order, dim3(1), dim3(1024), 0, stream, w.seg_start, w.counters,
                      w.seg_order, w.batch_state, w.batch_cnt, w.batch_rq, w.block_min,
                      w.resolve_blocks - w.team_blocks - w.helpers, 1);

@@ -332,6 +332,13 @@ int render_sharded(rc_group& g, const rc_scene* s, int W, int H, const rc_option
     }
     if (root->frames_all.ensure((size_t)G * block_bytes) || root->small_all.ensure((size_t)G * 16))
       return -1;
+    // parity: the root's own phase A writes its DEP lines and writer carries straight into the
+    // resolver's image-indexed buffers (W*H + 1 pixels), so its entries never travel or unpack
+    if (parity && (root->rootfb.deprec.ensure((P + 1) * rc::deprec_bytes()) ||
+                   root->rootfb.wcarry.ensure((P + 1) * sizeof(float4)))) {
+      std::fprintf(stderr, "Error: out of device memory for the root's resolver workspace\n");
+      return -1;
+    }
     HIP_TRY(hipEventRecord(root->ev[0], root->stream));
   }
   std::vector<rc::LaunchScene> ls(g.ranks.size());
@@ -362,8 +369,11 @@ int render_sharded(rc_group& g, const rc_scene* s, int W, int H, const rc_option
       std::fprintf(stderr, "Error: out of device memory for the shard workspace\n");
       return -1;
     }
+    const bool thin = &r == root;
     HIP_TRY(rc::launch_shard_local(ls[i], W, H, r.rank, G, r.nrows, maxrec, (uint8_t*)r.frame.p,
-                                   w[i], r.ent.p, r.rows.p, zc, r.stream));
+                                   w[i], r.ent.p, r.rows.p, zc, r.stream,
+                                   thin ? root->rootfb.deprec.p : nullptr,
+                                   thin ? (float4*)root->rootfb.wcarry.p : nullptr));
     HIP_TRY(hipMemcpyAsync(r.small.p, w[i].counters + 2, sizeof(int), hipMemcpyDeviceToDevice,
                            r.stream));
     HIP_TRY(hipEventRecord(r.rev[1], r.stream));
@@ -489,7 +499,7 @@ int render_sharded(rc_group& g, const rc_scene* s, int W, int H, const rc_option
       HIP_TRY(rc::launch_shard_resolve(ls[0], W, H, G, rmax, root->rows_all.p, root->ent_all.p,
                                        root->ent.p, offs.data(), maxrec, wr, img, rz,
                                        root->stream, rev,
-                                       fixed ? (int)per_rank : 0x7fffffff));
+                                       fixed ? (int)per_rank : 0x7fffffff, 1));
       HIP_TRY(hipEventRecord(root->ev[4], root->stream));
       if (d_image != img)
         HIP_TRY(hipMemcpyAsync(d_image, img, P * 3, hipMemcpyDeviceToDevice, root->stream));
