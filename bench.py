@@ -73,7 +73,7 @@ def load_pkg():
 
 # rocprofv3 --pmc summaries of this exact configuration from HEAD (scripts/pmc_valu.sh,
 # scripts/pmc_fast.sh -> scripts/pmc_summary.py): per-kernel counter means per launch.
-PMC_PROFILES = {("quadric", 4096, 6, "parity"): "profiles/r03e_pmc_lone_4096.json",
+PMC_PROFILES = {("quadric", 4096, 6, "parity"): "profiles/r04l_pmc_lone_4096.json",
                 ("reflection", 2048, 4, "parity"): "profiles/r03e_pmc_lone_c3.json",
                 ("quadric", 8192, 6, "parity"): "profiles/r03e_pmc_lone_c5.json",
                 ("quadric", 4096, 6, "fast"): "profiles/r02c_pmc_fast_4096.json"}
@@ -653,6 +653,9 @@ def main():
                          "traffic_unit": "bytes per launch (HBM, PMC)",
                          "valu_busy": pmc["valu_busy"] if pmc else None,
                          "frac_wait_any": pmc.get("frac_wait_any") if pmc else None,
+                         "valu_busy_basis": ("all 256 CUs (a pipeline lane's resolver holds 64 of "
+                                             "them: x4 for its own CUs)" if piped else
+                                             "all 256 CUs"),
                          "pmc_source": pmc_src,
                          "note": ("serial carry chain: latency-bound, see DESIGN.md; frac = per "
                                   "launch, frac_per_step = one image's work over ms_per_step"

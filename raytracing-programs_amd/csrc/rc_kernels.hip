@@ -79,15 +79,18 @@ static_assert(kTileW % 8 == 0 && kTileH % 8 == 0, "8x8 wave tiles");
 #ifndef RC_XCD_TILES
 #define RC_XCD_TILES 2   // measured: k_phase_a WRITE_SIZE 312 -> 269 MB in flight, time within noise
 #endif
+// order: RC_XCD_TILES for k_phase_a; k_render keeps the grid order (its only stores are the
+// framebuffer's; fast mode 0.64 ms in round 3 against 0.65-0.66 ms with chunks, r04l)
+template <int kOrder = RC_XCD_TILES>
 __device__ __forceinline__ void xcd_tile(int& bx, int& by) {
   const int nx = gridDim.x, n = nx * (int)gridDim.y;
   const int lin = (int)blockIdx.y * nx + (int)blockIdx.x;
   int t = lin;
-  if (RC_XCD_TILES == 1) {
+  if (kOrder == 1) {
     const int xcd = lin & 7, k = lin >> 3, q = n >> 3, r = n & 7;
     // XCDs below r take q + 1 tiles, the others q: a bijection of [0, n)
     t = xcd < r ? xcd * (q + 1) + k : r * (q + 1) + (xcd - r) * q + k;
-  } else if (RC_XCD_TILES == 2 && lin < (n & ~63)) {
+  } else if (kOrder == 2 && lin < (n & ~63)) {
     // the XCD's k-th workgroup -> chunk (k / 8) * 8 + xcd, tile k % 8 of it (a bijection of
     // the first n & ~63 tiles; the rest keep the grid order)
     const int xcd = lin & 7, k = lin >> 3;
@@ -240,7 +243,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_
   int lx, ly;
   tile_pixel(lx, ly);
   int bx, by;
-  xcd_tile(bx, by);
+  xcd_tile<0>(bx, by);
   const int x0 = bx * kTileW, r0 = by * kTileH;
   const int x = x0 + lx;
   const int r = r0 + ly;           // local (shard) row
