@@ -315,6 +315,13 @@ typedef struct rc_tuning {
                              cooperative steps and the team's next SCAN round is one
                              cooperative step of every team wave (default); 0: the leader's
                              LANE passes and LANE-only SCAN rounds                            */
+  int pipe_order;         /* frames in flight: creation order of the CU-masked streams (the
+                             runtime maps streams onto hardware queues in creation order): 0
+                             lane by lane (resolver, phase C), then the pixel streams; 1
+                             resolvers, pixel streams, phase C; 2 pixel streams, phase C,
+                             resolvers                                                        */
+  int pipe_helpers;       /* frames in flight: dense-run helper workgroups per resolver lane
+                             (0 = none, the default)                                          */
 } rc_tuning;
 void rc_default_tuning(rc_tuning *t);
 int rc_set_tuning(const rc_tuning *t);

@@ -68,6 +68,8 @@ rc_tuning default_tuning() {
   t.resolve_clean = 1;
   t.shard_lone = 1;
   t.team_cscan = 1;
+  t.pipe_order = 0;
+  t.pipe_helpers = 0;
   // regular segments of >= 3000 entries on whole workgroups when there are workgroups for all
   // of them (k_seg_order): lone quadric 4096^2 5.19 -> 5.06 ms (its ~100 3856-entry segments
   // 4.4 -> 2.5 ms, under the team segment); 8192^2 and pipeline lanes have more such segments
@@ -426,6 +428,7 @@ int rc_set_tuning(const rc_tuning* t) {
       in(t->comp_stream, 0, 2) && in(t->side_blocks, 0, 1 << 16) &&
       in(t->block_min, 0, 1 << 30) && in(t->pipe_inres, 0, 2) && in(t->x0, 0, 1) &&
       in(t->resolve_clean, 1, 64) && in(t->shard_lone, 0, 1) && in(t->team_cscan, 0, 1) &&
+      in(t->pipe_order, 0, 3) && in(t->pipe_helpers, 0, rc::kDenseSlots) &&
       !(t->split_shade && !t->side);
   if (!ok) {
     std::fprintf(stderr, "Error: rc_set_tuning: a field is out of range\n");
@@ -441,7 +444,7 @@ int rc_set_tuning(const rc_tuning* t) {
     if (!c.pipe.init) continue;
     if (t->pipe_resolvers != c.pipe.built_lanes || t->pipe_slots != c.pipe.built_slots ||
         t->pipe_res_cus != c.pipe.built_res || (t->pipe_timing != 0) != c.pipe.rt_on ||
-        (t->pipe_slotstreams == 0) != c.pipe.fifo) {
+        (t->pipe_slotstreams == 0) != c.pipe.fifo || t->pipe_order != c.pipe.built_order) {
       std::fprintf(stderr, "Warning: rc_set_tuning: the pipe_* fields take effect when device "
                    "%d's frame pipeline is rebuilt (rc_pipe_reset)\n", c.device);
       break;
@@ -683,7 +686,7 @@ int ensure_parity(DevCtx& c, FrameBufs& b, int W, int H, rc::ParityWork& w, int 
   // whose regular waves need those slots more (frames in flight without helpers: reflection
   // 2048^2 d4 7.5e9 -> 8.0e9 rays/s, quadric 8192^2 8.3e9 -> 8.8e9, quadric 4096^2 +1 %,
   // scripts/helper_sweep.sh)
-  w.helpers = piped ? 0 : tu.helpers;
+  w.helpers = piped ? tu.pipe_helpers : tu.helpers;
   if (w.helpers < 0) w.helpers = 0;
   if (w.helpers > rc::kDenseSlots) w.helpers = rc::kDenseSlots;   // one ring slot per helper
   if (w.team_blocks + w.helpers > w.resolve_blocks * 3 / 4) w.helpers = 0;
@@ -1065,6 +1068,10 @@ void pipe_release(DevCtx& c) {
   }
   for (int r = 0; r < Pipe::kLanes; ++r) p.pc[r] = nullptr;
   p.comp[0] = p.comp[1] = nullptr;
+  for (auto& sp : p.spare) {
+    if (sp) (void)hipStreamDestroy(sp);
+    sp = nullptr;
+  }
 }
 
 void pipe_release_all() {
@@ -1103,21 +1110,61 @@ int pipe_init(DevCtx& c, long long pixels) {
   const int words = (c.cus + 31) / 32;
   std::vector<uint32_t> ma(words, 0), mb(words, 0);
   for (int i = 0; i < c.cus; ++i) (i < res ? ma : mb)[i / 32] |= 1u << (i % 32);
-  for (int r = 0; r < p.lanes; ++r) {
-    HIP_TRY(hipExtStreamCreateWithCUMask(&p.res[r], (uint32_t)words, ma.data()));
-    // compaction off the pixel partition (any CU, first): quadric 8192^2 8.38e9 -> 8.49e9
-    // rays/s; at 4096^2 its workgroups on the resolver partition cost more (5.91e9 -> 5.85e9)
-    const bool comp = tu.comp_stream == 1 || (tu.comp_stream == 2 && pixels >= (32ll << 20));
-    if (r < 2 && comp) {
-      int lo = 0, hi = 0;
-      HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
-      HIP_TRY(hipStreamCreateWithPriority(&p.comp[r], hipStreamNonBlocking, hi));
+  // the CU-masked streams, in the order tu.pipe_order names (the runtime assigns hardware
+  // queues in creation order, and a queue's dispatcher serves one kernel's workgroups at a time)
+  const bool comp = tu.comp_stream == 1 || (tu.comp_stream == 2 && pixels >= (32ll << 20));
+  auto mk_res = [&]() -> int {
+    for (int r = 0; r < p.lanes; ++r) {
+      HIP_TRY(hipExtStreamCreateWithCUMask(&p.res[r], (uint32_t)words, ma.data()));
+      // compaction off the pixel partition (any CU, first): quadric 8192^2 8.38e9 -> 8.49e9
+      // rays/s; at 4096^2 its workgroups on the resolver partition cost more (5.91e9 -> 5.85e9)
+      if (r < 2 && comp) {
+        int lo = 0, hi = 0;
+        HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        HIP_TRY(hipStreamCreateWithPriority(&p.comp[r], hipStreamNonBlocking, hi));
+      }
     }
-    if (p.fifo) HIP_TRY(hipExtStreamCreateWithCUMask(&p.pc[r], (uint32_t)words, mb.data()));
+    return 0;
+  };
+  auto mk_pc = [&]() -> int {
+    for (int r = 0; r < p.lanes; ++r)
+      if (p.fifo) HIP_TRY(hipExtStreamCreateWithCUMask(&p.pc[r], (uint32_t)words, mb.data()));
+    return 0;
+  };
+  auto mk_pix = [&]() -> int {
+    for (int k = 0; k < p.slots; ++k)
+      if (!p.fifo || k < 2)
+        HIP_TRY(hipExtStreamCreateWithCUMask(&p.pix[k], (uint32_t)words, mb.data()));
+    return 0;
+  };
+  if (tu.pipe_order == 0) {   // lane by lane (resolver, its phase C), then the pixel streams
+    for (int r = 0; r < p.lanes; ++r) {
+      HIP_TRY(hipExtStreamCreateWithCUMask(&p.res[r], (uint32_t)words, ma.data()));
+      if (r < 2 && comp) {
+        int lo = 0, hi = 0;
+        HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        HIP_TRY(hipStreamCreateWithPriority(&p.comp[r], hipStreamNonBlocking, hi));
+      }
+      if (p.fifo) HIP_TRY(hipExtStreamCreateWithCUMask(&p.pc[r], (uint32_t)words, mb.data()));
+    }
+    if (mk_pix()) return -1;
+  } else if (tu.pipe_order == 1) {
+    if (mk_res() || mk_pix() || mk_pc()) return -1;
+  } else if (tu.pipe_order == 3 && p.fifo && p.lanes == 2) {
+    // four hardware queues dealt in creation order: each resolver lane alone on its queue
+    // (with an idle placeholder stream), the two pixel streams on one (their phase A run one
+    // at a time anyway) and the two phase C streams on the other
+    if (mk_res()) return -1;
+    HIP_TRY(hipExtStreamCreateWithCUMask(&p.pix[0], (uint32_t)words, mb.data()));
+    HIP_TRY(hipExtStreamCreateWithCUMask(&p.pc[0], (uint32_t)words, mb.data()));
+    for (int r = 0; r < 2; ++r)
+      HIP_TRY(hipExtStreamCreateWithCUMask(&p.spare[r], (uint32_t)words, ma.data()));
+    HIP_TRY(hipExtStreamCreateWithCUMask(&p.pix[1], (uint32_t)words, mb.data()));
+    HIP_TRY(hipExtStreamCreateWithCUMask(&p.pc[1], (uint32_t)words, mb.data()));
+  } else {
+    if (mk_pix() || mk_pc() || mk_res()) return -1;
   }
   for (int k = 0; k < p.slots; ++k) {
-    if (!p.fifo || k < 2)
-      HIP_TRY(hipExtStreamCreateWithCUMask(&p.pix[k], (uint32_t)words, mb.data()));
     HIP_TRY(hipEventCreateWithFlags(&p.adone[k], hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&p.ready[k], hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&p.done[k], hipEventDisableTiming));
@@ -1131,6 +1178,7 @@ int pipe_init(DevCtx& c, long long pixels) {
   p.built_lanes = tu.pipe_resolvers;
   p.built_slots = tu.pipe_slots;
   p.built_res = tu.pipe_res_cus;
+  p.built_order = tu.pipe_order;
   p.init = true;
   return 0;
 }

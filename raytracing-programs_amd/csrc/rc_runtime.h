@@ -134,6 +134,7 @@ struct Pipe {
   hipEvent_t ready[kSlots] = {}, done[kSlots] = {};
   bool fifo = true;                  // pa = pix[0] + pc[] (false: RC_PIPE_SLOTSTREAMS)
   hipStream_t pc[kLanes] = {};
+  hipStream_t spare[2] = {};         // pipe_order 3: placeholders that keep a queue per lane
   hipEvent_t cdone[kSlots] = {};
   bool cpend[kSlots] = {};           // slot k's phase C is enqueued and not yet synchronised
   hipEvent_t adone[kSlots] = {};     // after slot k's phase A
@@ -146,7 +147,7 @@ struct Pipe {
   long long last = -1;               // slot of the last parity frame
   bool used[kSlots] = {};
   bool rt_on = true;                 // resolver timing events recorded (RC_PIPE_NO_RT: off)
-  int built_lanes = 0, built_slots = 0, built_res = 0;   // the tuning this pipeline was built with
+  int built_lanes = 0, built_slots = 0, built_res = 0, built_order = 0;   // the tuning it was built with
   FrameLog log;                      // every pipelined parity frame, in submission order
 };
 
