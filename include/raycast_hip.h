@@ -321,7 +321,7 @@ typedef struct rc_tuning {
                              resolvers, pixel streams, phase C; 2 pixel streams, phase C,
                              resolvers                                                        */
   int pipe_helpers;       /* frames in flight: dense-run helper workgroups per resolver lane
-                             (0 = none, the default)                                          */
+                             (default 4; 0 = none)                                            */
 } rc_tuning;
 void rc_default_tuning(rc_tuning *t);
 int rc_set_tuning(const rc_tuning *t);

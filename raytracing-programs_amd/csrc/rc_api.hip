@@ -69,7 +69,8 @@ rc_tuning default_tuning() {
   t.shard_lone = 1;
   t.team_cscan = 1;
   t.pipe_order = 0;
-  t.pipe_helpers = 0;
+  t.pipe_helpers = 4;   // round 4: frames in flight 6.70-6.81e9 -> 6.83-6.90e9 at C4, C5 / C3 /
+                        // simple 1024^2 +0.8 / +1.2 / +2.3 % (profiles/r04q_pipe_helpers_*.txt)
   // regular segments of >= 3000 entries on whole workgroups when there are workgroups for all
   // of them (k_seg_order): lone quadric 4096^2 5.19 -> 5.06 ms (its ~100 3856-entry segments
   // 4.4 -> 2.5 ms, under the team segment); 8192^2 and pipeline lanes have more such segments
@@ -681,11 +682,10 @@ int ensure_parity(DevCtx& c, FrameBufs& b, int W, int H, rc::ParityWork& w, int 
     c.lone_lds = w.resolve_lds;
     c.lone_team = w.team_blocks;
   }
-  // helper blocks for handed-off dense runs (k_resolve): 8 of the grid for a lone frame
-  // (quadric 4096^2 5.85 -> 5.64 ms); none in a pipeline lane, whose grid is a partition's and
-  // whose regular waves need those slots more (frames in flight without helpers: reflection
-  // 2048^2 d4 7.5e9 -> 8.0e9 rays/s, quadric 8192^2 8.3e9 -> 8.8e9, quadric 4096^2 +1 %,
-  // scripts/helper_sweep.sh)
+  // helper blocks for handed-off dense runs (k_resolve): 16 of the grid for a lone frame,
+  // runs handed off after 128 changes (quadric 4096^2 5.01 -> 4.65 ms); 4 in a pipeline lane
+  // (pipe_helpers), whose grid is a partition's and whose regular waves need most of the slots
+  // (round 2, hand-offs after 512 changes: 8 helpers per lane lost 1-6 %)
   w.helpers = piped ? tu.pipe_helpers : tu.helpers;
   if (w.helpers < 0) w.helpers = 0;
   if (w.helpers > rc::kDenseSlots) w.helpers = rc::kDenseSlots;   // one ring slot per helper

@@ -284,7 +284,11 @@ PIPES = {"default": {},
          "one-lane-small-a": dict(pipe_resolvers=1, pipe_res_cus=32, pipe_timing=0),
          "one-wg-per-cu": dict(resolve_lds_kb=96, team_blocks=24),
          "phase-c-in-lanes": dict(pipe_inres=1),
-         "phase-c-in-lanes-until-done": dict(pipe_inres=2, pipe_slotstreams=1)}
+         "phase-c-in-lanes-until-done": dict(pipe_inres=2, pipe_slotstreams=1),
+         "no-lane-helpers": dict(pipe_helpers=0),
+         "lane-helpers-every-run": dict(pipe_helpers=8, hand_run=2),
+         "stream-order-1": dict(pipe_order=1),
+         "queue-per-lane": dict(pipe_order=3)}
 
 
 @pytest.mark.parametrize("pipe", list(PIPES))
