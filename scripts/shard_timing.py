@@ -12,6 +12,8 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 from helpers import rc, scene_path  # noqa: E402
 
 s = rc.Scene.from_file(scene_path("quadric"))
+# the exchange path at every G (a one-rank group otherwise renders a lone frame)
+rc.set_tuning(shard_lone=int(os.environ.get("SHARD_LONE", "0")))
 for n in (4096, 8192):
     out = torch.empty((n, n, 3), dtype=torch.uint8, device="cuda")
     for G, tr in ((1, "rccl"), (2, "copy"), (4, "copy"), (8, "copy")):
