@@ -69,7 +69,8 @@ rc_tuning default_tuning() {
   t.shard_lone = 1;
   t.team_cscan = 1;
   t.pipe_order = 0;
-  t.pipe_helpers = 4;   // round 4: frames in flight 6.70-6.81e9 -> 6.83-6.90e9 at C4, C5 / C3 /
+  t.pipe_helpers = 4;
+  t.patch_host = 0;   // round 4: frames in flight 6.70-6.81e9 -> 6.83-6.90e9 at C4, C5 / C3 /
                         // simple 1024^2 +0.8 / +1.2 / +2.3 % (profiles/r04q_pipe_helpers_*.txt)
   // regular segments of >= 3000 entries on whole workgroups when there are workgroups for all
   // of them (k_seg_order): lone quadric 4096^2 5.19 -> 5.06 ms (its ~100 3856-entry segments
@@ -356,6 +357,23 @@ int ensure_pinned(DevCtx& c, size_t entries) {
   return 0;
 }
 
+// patch_host: the DEP entries' packed colours go straight to pinned, mapped host memory from
+// phase C's stores (a batch of 64 entries is one 256-byte write), during the resolver, instead
+// of an 11 MB copy (quadric 4096^2) after the frame's last kernel.
+int ensure_host_patch(DevCtx& c, size_t entries) {
+  if (entries <= c.host_patch_entries) return 0;
+  if (c.host_patch) (void)hipHostFree(c.host_patch);
+  c.host_patch = c.host_patch_dev = nullptr;
+  c.host_patch_entries = 0;
+  HIP_TRY(hipHostMalloc((void**)&c.host_patch, entries * sizeof(uint32_t),
+                        hipHostMallocMapped | hipHostMallocCoherent));
+  void* d = nullptr;
+  HIP_TRY(hipHostGetDevicePointer(&d, c.host_patch, 0));
+  c.host_patch_dev = (uint32_t*)d;
+  c.host_patch_entries = entries;
+  return 0;
+}
+
 // The parity render's device-to-host copy, overlapped with the render (the
 // drop-in rate spans upload + kernels + copy).  Once phase A and the compaction are done
 // (ev[2]), every pixel except the DEP pixels is final: the framebuffer streams out on the copy
@@ -363,7 +381,7 @@ int ensure_pinned(DevCtx& c, size_t entries) {
 // phase C (ev[4]) only the DEP entries' packed colours follow (4 B per entry, ~17 % of the
 // pixels), and the host pool scatters them over the copy.
 int copy_overlapped(DevCtx& c, uint8_t* host, const uint8_t* dev, size_t bytes,
-                    const hipEvent_t* ev) {
+                    const hipEvent_t* ev, const uint32_t* host_patch) {
   if (ensure_pinned(c, 0)) return -1;
   HIP_TRY(hipEventSynchronize(ev[2]));
   HIP_TRY(hipMemcpyAsync(c.pin_cnt, c.fb.counters.p, 4 * sizeof(int), hipMemcpyDeviceToHost,
@@ -377,11 +395,16 @@ int copy_overlapped(DevCtx& c, uint8_t* host, const uint8_t* dev, size_t bytes,
   if (copy_to_host(c, host, dev, bytes, c.d2h)) return -1;
   HIP_TRY(hipEventSynchronize(ev[4]));
   if (!ndep) return 0;
-  HIP_TRY(hipMemcpyAsync(c.pin_patch, c.patch.p, ndep * sizeof(uint32_t), hipMemcpyDeviceToHost,
-                         c.d2h));
-  HIP_TRY(hipStreamSynchronize(c.d2h));
+  const uint32_t* rgb = host_patch;   // written by phase C itself (patch_host)
+  if (!rgb) {
+    HIP_TRY(hipMemcpyAsync(c.pin_patch, c.patch.p, ndep * sizeof(uint32_t),
+                           hipMemcpyDeviceToHost, c.d2h));
+    HIP_TRY(hipStreamSynchronize(c.d2h));
+    rgb = (const uint32_t*)c.pin_patch;
+  } else {
+    HIP_TRY(hipStreamSynchronize(c.d2h));   // the DEP list's copy
+  }
   const long long* pix = (const long long*)c.pin_pix;
-  const uint32_t* rgb = (const uint32_t*)c.pin_patch;
   HostPool::get().run([&](int part, int parts) {
     const size_t per = (ndep + parts - 1) / parts;
     const size_t a = (size_t)part * per, b = a + per < ndep ? a + per : ndep;
@@ -430,6 +453,7 @@ int rc_set_tuning(const rc_tuning* t) {
       in(t->block_min, 0, 1 << 30) && in(t->pipe_inres, 0, 2) && in(t->x0, 0, 1) &&
       in(t->resolve_clean, 1, 64) && in(t->shard_lone, 0, 1) && in(t->team_cscan, 0, 1) &&
       in(t->pipe_order, 0, 3) && in(t->pipe_helpers, 0, rc::kDenseSlots) &&
+      in(t->patch_host, 0, 1) &&
       !(t->split_shade && !t->side);
   if (!ok) {
     std::fprintf(stderr, "Error: rc_set_tuning: a field is out of range\n");
@@ -1486,11 +1510,16 @@ int rc_render(const rc_scene* s, int W, int H, const rc_options* opt, uint8_t* p
   // colours to phase C, so its framebuffer is not final after phase A
   const bool overlap = parity && !tune().split_shade && tune().overlap_d2h;
   uint32_t* patch = nullptr;
+  const bool hpatch = overlap && tune().patch_host;
   if (overlap) {
-    if ((!c->d2h && hipStreamCreateWithFlags(&c->d2h, hipStreamNonBlocking) != hipSuccess) ||
-        c->patch.ensure((size_t)W * H * sizeof(uint32_t)))
-      return -1;
-    patch = (uint32_t*)c->patch.p;
+    if (!c->d2h && hipStreamCreateWithFlags(&c->d2h, hipStreamNonBlocking) != hipSuccess) return -1;
+    if (hpatch) {
+      if (ensure_host_patch(*c, (size_t)W * H)) return -1;
+      patch = c->host_patch_dev;
+    } else {
+      if (c->patch.ensure((size_t)W * H * sizeof(uint32_t))) return -1;
+      patch = (uint32_t*)c->patch.p;
+    }
   }
   hipEvent_t* ev = nullptr;
   const long long own = c->lone_log.head;   // this frame's ring entry (parity frames log one)
@@ -1498,7 +1527,9 @@ int rc_render(const rc_scene* s, int W, int H, const rc_options* opt, uint8_t* p
   prefault(pixmap, (size_t)H * row_bytes);
   auto td = std::chrono::steady_clock::now();
   if (overlap) {
-    if (copy_overlapped(*c, pixmap, d_out, (size_t)H * row_bytes, ev)) return -1;
+    if (copy_overlapped(*c, pixmap, d_out, (size_t)H * row_bytes, ev,
+                        hpatch ? c->host_patch : nullptr))
+      return -1;
   } else if (copy_to_host(*c, pixmap, d_out, (size_t)H * row_bytes, c->stream)) {
     return -1;
   }

@@ -186,6 +186,9 @@ struct DevCtx {
   uint8_t* pin_patch = nullptr;   // pinned: DEP entries' packed RGB
   size_t pin_bytes = 0;           // capacity of each pinned buffer, in entries
   int* pin_cnt = nullptr;         // pinned: counters[0..3]
+  uint32_t* host_patch = nullptr;     // pinned, mapped: phase C's packed RGB per DEP entry
+  uint32_t* host_patch_dev = nullptr; // its device address (patch_host)
+  size_t host_patch_entries = 0;
   FrameLog lone_log;   // every parity frame rendered in `fb` (rc_render, rc_render_device)
   // rc_resolver_stats: the last rc_frames_wait window's record (frames in flight), and the
   // resolver placement of the last frame of each kind (grid, CUs it may use)
@@ -212,6 +215,7 @@ int ctx_get(int device, DevCtx** out);
 int fill_resolver_stats(DevCtx& c, const FrameLog::Diag& d, int grid, int res_cus, int lds,
                         int team, rc_resolver_stats* r);
 int copy_to_host(DevCtx& c, uint8_t* host, const uint8_t* dev, size_t bytes, hipStream_t st);
+int ensure_host_patch(DevCtx& c, size_t entries);
 void prefault(uint8_t* p, size_t n);
 int upload_scene(FrameBufs& b, hipStream_t stream, const rc_scene* s, rc::LaunchScene& ls);
 int ensure_parity(DevCtx& c, FrameBufs& b, int W, int H, rc::ParityWork& w, int res_cus,
