@@ -12,7 +12,11 @@ for the kernels (test infrastructure).
   which rebuilds the image's scan order and segment table from the records alone
   (k_shard_rows / k_row_scan / k_shard_unpack), resolves the chain and shades every DEP entry
   into the de-interleaved image itself (phase C inside the root's resolver); nothing returns
-  to the ranks.  The image must equal the oracle's whole-image render."""
+  to the ranks.  Rank 0's own rows never travel (round 4): its phase A keeps its writer
+  carry-outs at their image pixels — only the key writers of each 8-pixel tile row
+  (k_phase_a writer_may_key) — and its entries are thin {image pixel, in-row writer} pairs whose
+  carries the root looks up there; its row block is de-interleaved in place.  The image must
+  equal the oracle's whole-image render."""
 import ctypes
 import os
 import socket
@@ -57,12 +61,29 @@ def pixels(scene, W, H, depth, mode, pix, cin=None):
     return rgb, cout, cls, z
 
 
+def key_writers(cls):
+    """k_phase_a writer_may_key over one image row: a writer's carry-out is stored unless a
+    later writer of its 8-pixel tile row follows with no DEP pixel between them."""
+    W = len(cls)
+    keep = np.zeros(W, bool)
+    for x0 in range(0, W, 8):
+        frag = [int(cls[x]) if x < W else -1 for x in range(x0, x0 + 8)]
+        for l in range(8):
+            if x0 + l < W and frag[l] == WRITER:
+                nxt = [j for j in range(l + 1, 8) if frag[j] == WRITER]
+                keep[x0 + l] = not nxt or any(frag[j] >= 2 for j in range(l + 1, nxt[0]))
+    return keep
+
+
 def rank_phase_a(scene, W, H, depth, rank, G):
-    """A rank's phase A and wire records (k_phase_a + k_shard_pack)."""
+    """A rank's phase A and wire records (k_phase_a + k_shard_pack).  Rank 0 (thin): entries
+    are (image pixel, in-row writer) and its key writers' carry-outs stay in `carry` at their
+    image pixels (the root resolver's own buffers)."""
     rows = list(range(rank, H, G))
     local = np.zeros((len(rows), W, 3), np.uint8)
     entries, summaries = [], []
     dep_pix = []
+    carry = {}
     zero = 0
     for j, y in enumerate(rows):
         pix = np.arange(W, dtype=np.int64) + y * W
@@ -70,6 +91,9 @@ def rank_phase_a(scene, W, H, depth, rank, G):
         dep = cls >= 2
         local[j][~dep] = rgb[~dep]
         zero += int(z[~dep].sum())
+        if rank == 0:
+            for x in np.nonzero(key_writers(cls))[0]:
+                carry[y * W + int(x)] = cout[x]
         lw = ld = wf = -1
         nst = 0
         first = True
@@ -79,23 +103,30 @@ def rank_phase_a(scene, W, H, depth, rank, G):
                     wf, first = lw, False
                 elif lw > ld:
                     nst += 1   # a writer between the previous DEP and this one
-                kc = cout[lw] if lw >= 0 else np.zeros(3, np.float32)
-                entries.append((y * W + x, y * W + lw if lw >= 0 else -1, kc))
+                if rank == 0:   # thin: the carry is read at the writer's image pixel
+                    entries.append((y * W + x, y * W + lw if lw >= 0 else -1))
+                else:
+                    kc = cout[lw] if lw >= 0 else np.zeros(3, np.float32)
+                    entries.append((y * W + x, y * W + lw if lw >= 0 else -1, kc))
                 dep_pix.append((j, x))
                 ld = x
             elif cls[x] == WRITER:
                 lw = x
+        if rank == 0 and lw >= 0:   # the root reads its row-last writer's carry in place
+            assert y * W + lw in carry, "a row's last writer is a key writer"
         summaries.append({"ndep": int(dep.sum()), "nstart": nst,
                           "lastw": y * W + lw if lw >= 0 else -1,
                           "lastd": y * W + ld if ld >= 0 else -1,
                           "wfirst": y * W + wf if wf >= 0 else -1,
-                          "cw": cout[lw] if lw >= 0 else np.zeros(3, np.float32)})
-    return local, entries, summaries, dep_pix, zero
+                          "cw": (carry[y * W + lw] if rank == 0 else cout[lw]) if lw >= 0
+                          else np.zeros(3, np.float32)})
+    return local, entries, summaries, dep_pix, zero, carry
 
 
-def root_resolve(scene, W, H, depth, G, entries_all, rows_all):
-    """Rank 0: the image's scan order from the wire records alone, the segment table and the
-    exact chain (every DEP pixel's carry-in, in each rank's entry order)."""
+def root_resolve(scene, W, H, depth, G, entries_all, rows_all, root_carry):
+    """Rank 0: the image's scan order from the wire records alone (its own thin entries
+    with the carries its phase A kept), the segment table and the exact chain (every DEP
+    pixel's carry-in, in each rank's entry order)."""
     row_off, pw, pd = {}, -1, -1
     starts = []          # (global entry index, initial carry)
     order = []           # (rank, local index) in image scan order
@@ -105,7 +136,11 @@ def root_resolve(scene, W, H, depth, G, entries_all, rows_all):
         loff = sum(rows_all[g][q]["ndep"] for q in range(j))
         prev = pd
         for i in range(r["ndep"]):
-            pix, kin, kc = entries_all[g][loff + i]
+            if g == 0:
+                pix, kin = entries_all[0][loff + i]
+                kc = root_carry[kin] if kin >= 0 else None   # KeyError: a key writer dropped
+            else:
+                pix, kin, kc = entries_all[g][loff + i]
             kw = kin if kin >= 0 else pw
             if prev < 0 or kw > prev:
                 if kin >= 0:
@@ -149,20 +184,25 @@ def _worker(rank, world, port, name, W, H, depth, mode, result_path):
         send[:nrows] = torch.from_numpy(rgb.reshape(nrows, W, 3))
         zero = int(z.sum())
     else:
-        local, entries, summaries, dep_pix, zero = rank_phase_a(scene, W, H, depth, rank, world)
+        local, entries, summaries, dep_pix, zero, carry = rank_phase_a(scene, W, H, depth, rank,
+                                                                       world)
         gathered = [None] * world if rank == 0 else None
-        dist.gather_object((entries, summaries), gathered, dst=0)
-        send[:nrows] = torch.from_numpy(local)   # non-DEP pixels final after phase A
+        # rank 0's entries stay where they are: it contributes only its row summaries
+        dist.gather_object((entries if rank else None, summaries), gathered, dst=0)
+        if rank:
+            send[:nrows] = torch.from_numpy(local)   # non-DEP pixels final after phase A
     blocks = [torch.empty_like(send) for _ in range(world)] if rank == 0 else None
     dist.gather(send, blocks, dst=0)
     zs = [None] * world if rank == 0 else None
     dist.gather_object(zero, zs, dst=0)
     if rank == 0:
+        if mode == "parity":   # the root's own block is de-interleaved in place, never sent
+            blocks[0][:nrows] = torch.from_numpy(local)
         img = rc.deinterleave(torch.stack(blocks), H).numpy()
         zero_all = sum(zs)
         if mode == "parity":   # the root: the chain, then phase C of every DEP entry into img
-            ents = [g[0] for g in gathered]
-            cin = root_resolve(scene, W, H, depth, world, ents, [g[1] for g in gathered])
+            ents = [entries] + [g[0] for g in gathered[1:]]
+            cin = root_resolve(scene, W, H, depth, world, ents, [g[1] for g in gathered], carry)
             for g in range(world):
                 if not len(ents[g]):
                     continue
