@@ -87,7 +87,7 @@ PMC_TRAFFIC_INFLIGHT = {("quadric", 4096, 6, "parity"): "profiles/r03f_pmc_traff
 # The headline's whole counter set from ONE command at HEAD (scripts/pmc_headline.sh: kernel
 # stats, VALU/wave-state and FETCH/WRITE passes of `bench.py --timed-only --steps 20 --warmup
 # 3`, the default frames in flight): valu_busy and traffic of the headline line come from it.
-PMC_HEADLINE = {("quadric", 4096, 6, "parity"): "profiles/r04_pmc_headline.json"}
+PMC_HEADLINE = {("quadric", 4096, 6, "parity"): "profiles/r04b_pmc_headline.json"}
 
 
 def pmc_kernel(kernel, scene, size, depth, mode, inflight=False):

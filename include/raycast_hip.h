@@ -325,7 +325,7 @@ typedef struct rc_tuning {
   int patch_host;         /* rc_render (parity, overlap_d2h): phase C writes the DEP entries'
                              packed colours straight into pinned host memory (zero-copy), so
                              nothing is left to copy when the frame ends; 0: a device buffer
-                             copied after phase C                                             */
+                             copied after phase C (default 1)                                 */
 } rc_tuning;
 void rc_default_tuning(rc_tuning *t);
 int rc_set_tuning(const rc_tuning *t);

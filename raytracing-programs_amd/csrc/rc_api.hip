@@ -71,7 +71,7 @@ rc_tuning default_tuning() {
   t.pipe_order = 0;
   t.pipe_helpers = 4;   // round 4: frames in flight 6.70-6.81e9 -> 6.83-6.90e9 at C4, C5 / C3 /
                         // simple 1024^2 +0.8 / +1.2 / +2.3 % (profiles/r04q_pipe_helpers_*.txt)
-  t.patch_host = 0;
+  t.patch_host = 1;   // round 4: rc_render end to end 5.39-5.47 -> 5.29-5.33 ms (profiles/r04v_patch_ab.txt)
   // regular segments of >= 3000 entries on whole workgroups when there are workgroups for all
   // of them (k_seg_order): lone quadric 4096^2 5.19 -> 5.06 ms (its ~100 3856-entry segments
   // 4.4 -> 2.5 ms, under the team segment); 8192^2 and pipeline lanes have more such segments
