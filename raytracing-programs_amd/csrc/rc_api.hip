@@ -374,6 +374,28 @@ int ensure_host_patch(DevCtx& c, size_t entries) {
   return 0;
 }
 
+// RC_E2E_TRACE=1: rc_render prints its host-side marks (ms from entry) to stderr, to split the
+// end-to-end time into the enqueue, the wait for the device frame and what follows it.
+struct E2eTrace {
+  static bool on() {
+    static const bool v = std::getenv("RC_E2E_TRACE") != nullptr;
+    return v;
+  }
+  std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+  double at[8] = {};
+  void mark(int i) {
+    if (on()) at[i] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  }
+  void print() const {
+    if (on())
+      std::fprintf(stderr,
+                   "rc_e2e: enqueued %.3f prefaulted %.3f phaseA+compact %.3f copy %.3f frame %.3f "
+                   "scatter %.3f synced %.3f end %.3f\n",
+                   at[0], at[1], at[2], at[3], at[4], at[5], at[6], at[7]);
+  }
+};
+E2eTrace* g_e2e = nullptr;   // set for the duration of one traced rc_render (under c->mu)
+
 // The parity render's device-to-host copy, overlapped with the render (the
 // drop-in rate spans upload + kernels + copy).  Once phase A and the compaction are done
 // (ev[2]), every pixel except the DEP pixels is final: the framebuffer streams out on the copy
@@ -384,6 +406,7 @@ int copy_overlapped(DevCtx& c, uint8_t* host, const uint8_t* dev, size_t bytes,
                     const hipEvent_t* ev, const uint32_t* host_patch) {
   if (ensure_pinned(c, 0)) return -1;
   HIP_TRY(hipEventSynchronize(ev[2]));
+  if (g_e2e) g_e2e->mark(2);
   HIP_TRY(hipMemcpyAsync(c.pin_cnt, c.fb.counters.p, 4 * sizeof(int), hipMemcpyDeviceToHost,
                          c.d2h));
   HIP_TRY(hipStreamSynchronize(c.d2h));
@@ -393,7 +416,9 @@ int copy_overlapped(DevCtx& c, uint8_t* host, const uint8_t* dev, size_t bytes,
     HIP_TRY(hipMemcpyAsync(c.pin_pix, c.fb.dep_pix.p, ndep * sizeof(long long),
                            hipMemcpyDeviceToHost, c.d2h));
   if (copy_to_host(c, host, dev, bytes, c.d2h)) return -1;
+  if (g_e2e) g_e2e->mark(3);
   HIP_TRY(hipEventSynchronize(ev[4]));
+  if (g_e2e) g_e2e->mark(4);
   if (!ndep) return 0;
   const uint32_t* rgb = host_patch;   // written by phase C itself (patch_host)
   if (!rgb) {
@@ -416,6 +441,7 @@ int copy_overlapped(DevCtx& c, uint8_t* host, const uint8_t* dev, size_t bytes,
       q[2] = (uint8_t)(v >> 16);
     }
   });
+  if (g_e2e) g_e2e->mark(5);
   return 0;
 }
 
@@ -1523,8 +1549,16 @@ int rc_render(const rc_scene* s, int W, int H, const rc_options* opt, uint8_t* p
   }
   hipEvent_t* ev = nullptr;
   const long long own = c->lone_log.head;   // this frame's ring entry (parity frames log one)
+  E2eTrace trace;
+  trace.t0 = t0;
+  struct Unset {
+    ~Unset() { g_e2e = nullptr; }
+  } unset;
+  if (E2eTrace::on()) g_e2e = &trace;
   if (enqueue_render(*c, s, W, H, 0, 1, H, opt, d_out, c->stream, true, patch, &ev)) return -1;
+  trace.mark(0);
   prefault(pixmap, (size_t)H * row_bytes);
+  trace.mark(1);
   auto td = std::chrono::steady_clock::now();
   if (overlap) {
     if (copy_overlapped(*c, pixmap, d_out, (size_t)H * row_bytes, ev,
@@ -1536,6 +1570,7 @@ int rc_render(const rc_scene* s, int W, int H, const rc_options* opt, uint8_t* p
   // this frame's latched hand-off words: its own failure is reported by this call and
   // consumed; another stream's frame that failed meanwhile is left to the next call
   HIP_TRY(hipStreamSynchronize(c->stream));
+  trace.mark(6);
   if (c->lone_log.entry_failed(own)) {
     c->lone_log.poll();
     (void)check_spin_error(c->fb, opt);   // the details, while the workspace still holds them
@@ -1552,6 +1587,8 @@ int rc_render(const rc_scene* s, int W, int H, const rc_options* opt, uint8_t* p
   } else {
     fill_device_timing(*c, opt, nullptr);
   }
+  trace.mark(7);
+  trace.print();
   return 0;
 }
 
