@@ -70,6 +70,9 @@ def e2e(label, **tune):
         pkg.set_tuning(**{k: base[k] for k in tune})
 
 
+if os.environ.get("E2E_COPY_THREADS"):   # the host pool's size is fixed at its first use
+    pkg.set_tuning(copy_threads=int(os.environ["E2E_COPY_THREADS"]))
+    print(f"copy_threads {pkg.get_tuning()['copy_threads']}", flush=True)
 print(f"lone rc_render_device {lone():.3f} ms", flush=True)
 if os.environ.get("RC_E2E_TRACE"):   # host marks of each rep on stderr (rc_api.hip E2eTrace)
     e2e("default (traced)")
