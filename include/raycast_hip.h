@@ -324,8 +324,10 @@ typedef struct rc_tuning {
                              (default 4; 0 = none)                                            */
   int patch_host;         /* rc_render (parity, overlap_d2h): phase C writes the DEP entries'
                              packed colours straight into pinned host memory (zero-copy), so
-                             nothing is left to copy when the frame ends; 0: a device buffer
-                             copied after phase C (default 1)                                 */
+                             nothing is left to copy when the frame ends, and the host
+                             scatters each entry as it arrives, during the frame (default 2);
+                             1: scattered after the frame; 0: a device buffer copied after
+                             phase C                                                          */
 } rc_tuning;
 void rc_default_tuning(rc_tuning *t);
 int rc_set_tuning(const rc_tuning *t);

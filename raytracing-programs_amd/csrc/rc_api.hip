@@ -71,7 +71,8 @@ rc_tuning default_tuning() {
   t.pipe_order = 0;
   t.pipe_helpers = 4;   // round 4: frames in flight 6.70-6.81e9 -> 6.83-6.90e9 at C4, C5 / C3 /
                         // simple 1024^2 +0.8 / +1.2 / +2.3 % (profiles/r04q_pipe_helpers_*.txt)
-  t.patch_host = 1;   // round 4: rc_render end to end 5.39-5.47 -> 5.29-5.33 ms (profiles/r04v_patch_ab.txt)
+  t.patch_host = 2;   // round 4: rc_render end to end 5.39-5.47 (0) -> 5.29-5.33 (1) -> 5.02-5.07 ms
+                      // (profiles/r04v_patch_ab.txt, r04z_e2e_anatomy.txt)
   // regular segments of >= 3000 entries on whole workgroups when there are workgroups for all
   // of them (k_seg_order): lone quadric 4096^2 5.19 -> 5.06 ms (its ~100 3856-entry segments
   // 4.4 -> 2.5 ms, under the team segment); 8192^2 and pipeline lanes have more such segments
@@ -359,9 +360,17 @@ int ensure_pinned(DevCtx& c, size_t entries) {
 
 // patch_host: the DEP entries' packed colours go straight to pinned, mapped host memory from
 // phase C's stores (a batch of 64 entries is one 256-byte write), during the resolver, instead
-// of an 11 MB copy (quadric 4096^2) after the frame's last kernel.
+// of an 11 MB copy (quadric 4096^2) after the frame's last kernel.  Entries carry a ready mark
+// (kPatchReady), so for patch_host 2 the array must start the frame cleared: that scatter clears
+// what it consumes; patch_host 1's (and a frame that ended early) leave host_patch_dirty entries.
 int ensure_host_patch(DevCtx& c, size_t entries) {
-  if (entries <= c.host_patch_entries) return 0;
+  if (entries <= c.host_patch_entries) {
+    if (tune().patch_host == 2 && c.host_patch_dirty) {
+      std::memset(c.host_patch, 0, c.host_patch_dirty * sizeof(uint32_t));
+      c.host_patch_dirty = 0;
+    }
+    return 0;
+  }
   if (c.host_patch) (void)hipHostFree(c.host_patch);
   c.host_patch = c.host_patch_dev = nullptr;
   c.host_patch_entries = 0;
@@ -371,7 +380,48 @@ int ensure_host_patch(DevCtx& c, size_t entries) {
   HIP_TRY(hipHostGetDevicePointer(&d, c.host_patch, 0));
   c.host_patch_dev = (uint32_t*)d;
   c.host_patch_entries = entries;
+  std::memset(c.host_patch, 0, entries * sizeof(uint32_t));
+  c.host_patch_dirty = 0;
   return 0;
+}
+
+// The scatter of a mapped colour patch while the frame still runs (patch_host): each host
+// thread sweeps its share of the DEP list, scatters every entry phase C has marked ready and
+// clears it, until its share is done; once the frame's last kernel has completed (ev_done),
+// one more sweep takes everything left.  The framebuffer copy must already be in `host` (it
+// carries the DEP pixels' phase-A bytes, which the patch overwrites).
+void scatter_progressive(uint8_t* host, const long long* pix, uint32_t* patch, size_t ndep,
+                         hipEvent_t ev_done) {
+  std::atomic<bool> over{false};
+  HostPool::get().run([&](int part, int parts) {
+    const size_t per = (ndep + parts - 1) / parts;
+    const size_t a = (size_t)part * per, b = a + per < ndep ? a + per : ndep;
+    if (a >= b) return;
+    size_t left = b - a, lo = a;   // lo: entries below it are all consumed
+    for (;;) {
+      const bool last = over.load(std::memory_order_acquire);
+      size_t got = 0;
+      bool gap = false;
+      for (size_t j = lo; j < b; ++j) {
+        volatile uint32_t* e = patch + j;
+        const uint32_t v = *e;
+        if (!(v & rc::kPatchReady)) {
+          gap = true;
+          continue;
+        }
+        uint8_t* q = host + 3 * (size_t)pix[j];
+        q[0] = (uint8_t)v;
+        q[1] = (uint8_t)(v >> 8);
+        q[2] = (uint8_t)(v >> 16);
+        *e = 0;
+        ++got;
+        if (!gap) lo = j + 1;
+      }
+      left -= got;
+      if (!left || last) return;   // after the frame an unmarked entry stays unmarked
+      if (!got && hipEventQuery(ev_done) == hipSuccess) over.store(true, std::memory_order_release);
+    }
+  });
 }
 
 // RC_E2E_TRACE=1: rc_render prints its host-side marks (ms from entry) to stderr, to split the
@@ -401,9 +451,11 @@ E2eTrace* g_e2e = nullptr;   // set for the duration of one traced rc_render (un
 // (ev[2]), every pixel except the DEP pixels is final: the framebuffer streams out on the copy
 // stream while the carry resolver runs, together with the DEP list (pixel per entry).  After
 // phase C (ev[4]) only the DEP entries' packed colours follow (4 B per entry, ~17 % of the
-// pixels), and the host pool scatters them over the copy.
+// pixels), and the host pool scatters them over the copy — or, with patch_host, phase C wrote
+// them into mapped host memory and the pool scatters each as it arrives (scatter_progressive),
+// so only the frame's last entries are left once it ends.
 int copy_overlapped(DevCtx& c, uint8_t* host, const uint8_t* dev, size_t bytes,
-                    const hipEvent_t* ev, const uint32_t* host_patch) {
+                    const hipEvent_t* ev, uint32_t* host_patch) {
   if (ensure_pinned(c, 0)) return -1;
   HIP_TRY(hipEventSynchronize(ev[2]));
   if (g_e2e) g_e2e->mark(2);
@@ -417,17 +469,30 @@ int copy_overlapped(DevCtx& c, uint8_t* host, const uint8_t* dev, size_t bytes,
                            hipMemcpyDeviceToHost, c.d2h));
   if (copy_to_host(c, host, dev, bytes, c.d2h)) return -1;
   if (g_e2e) g_e2e->mark(3);
+  if (host_patch && ndep && tune().patch_host == 2) {   // consumed as it arrives
+    HIP_TRY(hipStreamSynchronize(c.d2h));   // the DEP list's copy
+    c.host_patch_dirty = std::max(c.host_patch_dirty, ndep);
+    scatter_progressive(host, (const long long*)c.pin_pix, host_patch, ndep, ev[4]);
+    HIP_TRY(hipEventSynchronize(ev[4]));
+    c.host_patch_dirty = 0;   // every entry below ndep consumed, none written above it
+    if (g_e2e) {
+      g_e2e->mark(4);
+      g_e2e->mark(5);
+    }
+    return 0;
+  }
   HIP_TRY(hipEventSynchronize(ev[4]));
   if (g_e2e) g_e2e->mark(4);
   if (!ndep) return 0;
-  const uint32_t* rgb = host_patch;   // written by phase C itself (patch_host)
-  if (!rgb) {
+  const uint32_t* rgb = host_patch;   // written by phase C itself (patch_host 1)
+  if (rgb) {
+    c.host_patch_dirty = std::max(c.host_patch_dirty, ndep);   // its ready marks stay
+    HIP_TRY(hipStreamSynchronize(c.d2h));   // the DEP list's copy
+  } else {
     HIP_TRY(hipMemcpyAsync(c.pin_patch, c.patch.p, ndep * sizeof(uint32_t),
                            hipMemcpyDeviceToHost, c.d2h));
     HIP_TRY(hipStreamSynchronize(c.d2h));
     rgb = (const uint32_t*)c.pin_patch;
-  } else {
-    HIP_TRY(hipStreamSynchronize(c.d2h));   // the DEP list's copy
   }
   const long long* pix = (const long long*)c.pin_pix;
   HostPool::get().run([&](int part, int parts) {
@@ -479,7 +544,7 @@ int rc_set_tuning(const rc_tuning* t) {
       in(t->block_min, 0, 1 << 30) && in(t->pipe_inres, 0, 2) && in(t->x0, 0, 1) &&
       in(t->resolve_clean, 1, 64) && in(t->shard_lone, 0, 1) && in(t->team_cscan, 0, 1) &&
       in(t->pipe_order, 0, 3) && in(t->pipe_helpers, 0, rc::kDenseSlots) &&
-      in(t->patch_host, 0, 1) &&
+      in(t->patch_host, 0, 2) &&
       !(t->split_shade && !t->side);
   if (!ok) {
     std::fprintf(stderr, "Error: rc_set_tuning: a field is out of range\n");

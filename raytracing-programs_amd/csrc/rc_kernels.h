@@ -94,6 +94,10 @@ hipError_t launch_parity(const LaunchScene& s, int W, int H, int maxrec, uint8_t
                          const ParityWork& w, unsigned long long* zcount, hipStream_t stream,
                          const hipEvent_t* ev);
 
+// Top byte of a colour-patch entry (ParityWork::patch) once phase C has stored it; the low three
+// bytes are R, G, B.  rc_render's host side consumes marked entries and clears them to 0.
+constexpr uint32_t kPatchReady = 0xFF000000u;
+
 // Phase C of a frame launched with defer_c: waits for w.rdone on `stream`.
 hipError_t launch_phase_c(const LaunchScene& s, int W, int H, int maxrec, uint8_t* out,
                           const ParityWork& w, unsigned long long* zcount, hipStream_t stream);

@@ -178,7 +178,9 @@ __device__ __forceinline__ void store_rgb(uint8_t* __restrict__ p, V3 c) {
 
 // Phase C's store of DEP entry j at pixel p: the framebuffer, and — when the host is copying
 // the framebuffer out while the resolver runs (rc_render) — the entry's packed RGB in `patch`,
-// which the host then scatters over the DEP pixels of its copy.
+// which the host then scatters over the DEP pixels of its copy.  The top byte is a ready mark
+// (kPatchReady): one 4-byte store carries colour and mark together, so a host reading mapped
+// memory during the frame scatters an entry as soon as it sees the mark, and clears it.
 __device__ __forceinline__ void store_dep(uint8_t* __restrict__ out, uint32_t* __restrict__ patch,
                                           long long p, int j, V3 c) {
   const uint8_t r = quant(c.x), g = quant(c.y), b = quant(c.z);
@@ -186,7 +188,7 @@ __device__ __forceinline__ void store_dep(uint8_t* __restrict__ out, uint32_t* _
   q[0] = r;
   q[1] = g;
   q[2] = b;
-  if (patch) patch[j] = (uint32_t)r | ((uint32_t)g << 8) | ((uint32_t)b << 16);
+  if (patch) patch[j] = kPatchReady | (uint32_t)r | ((uint32_t)g << 8) | ((uint32_t)b << 16);
 }
 
 __device__ __forceinline__ void flush_events(int zero_events, unsigned long long* counter) {

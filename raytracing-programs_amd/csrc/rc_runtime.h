@@ -189,6 +189,7 @@ struct DevCtx {
   uint32_t* host_patch = nullptr;     // pinned, mapped: phase C's packed RGB per DEP entry
   uint32_t* host_patch_dev = nullptr; // its device address (patch_host)
   size_t host_patch_entries = 0;
+  size_t host_patch_dirty = 0;       // entries below it may hold an earlier frame's ready mark
   FrameLog lone_log;   // every parity frame rendered in `fb` (rc_render, rc_render_device)
   // rc_resolver_stats: the last rc_frames_wait window's record (frames in flight), and the
   // resolver placement of the last frame of each kind (grid, CUs it may use)

@@ -76,10 +76,12 @@ if os.environ.get("E2E_COPY_THREADS"):   # the host pool's size is fixed at its 
 print(f"lone rc_render_device {lone():.3f} ms", flush=True)
 if os.environ.get("RC_E2E_TRACE"):   # host marks of each rep on stderr (rc_api.hip E2eTrace)
     e2e("default (traced)")
+    e2e("patch_host=1 (traced)", patch_host=1)
     sys.exit(0)
 e2e("default")
 e2e("prefault=0", prefault=0)
 e2e("patch_host=0", patch_host=0)
+e2e("patch_host=1", patch_host=1)
 e2e("overlap_d2h=0", overlap_d2h=0)
 e2e("default again")
 print(f"lone rc_render_device {lone():.3f} ms", flush=True)

@@ -73,6 +73,7 @@ SCHEDULES = {"no-side": dict(side=0), "side-always": dict(side=1), "side-by-size
              "small-grid": dict(resolve_grid=64, team_blocks=16),
              "serial-plain-d2h": dict(overlap_d2h=0, staged_d2h=0, prefault=0),
              "device-patch": dict(patch_host=0),
+             "mapped-patch-after-frame": dict(patch_host=1),
              "helpers-8-hand-run-512": dict(helpers=8, hand_run=512)}
 
 
@@ -89,7 +90,10 @@ def test_parity_schedules(sched, scenes, table):
     a hand-off to the helper blocks after every change (hand_run=1: the
     queue overflows), a single helper block, none, the lane-only evaluator (coop=0), a small
     resolver grid, the plain serial copy to the host, the colour patch through a device buffer
-    (patch_host=0: a device buffer copied after phase C) and the round-3 helper settings."""
+    (patch_host=0: a device buffer copied after phase C), the mapped patch scattered after the
+    frame instead of entry by entry during it (patch_host=1: its frames leave the mapped array
+    marked, so the next schedule's default frames also check that it is cleared before use) and
+    the round-3 helper settings."""
     with rc.tuned(**SCHEDULES[sched]):
         for key in ("quadric:4096x4096:d6:parity", "reflection:2048x2048:d4:parity",
                     "quadric:333x517:d6:parity"):
