@@ -473,6 +473,7 @@ int copy_overlapped(DevCtx& c, uint8_t* host, const uint8_t* dev, size_t bytes,
     HIP_TRY(hipStreamSynchronize(c.d2h));   // the DEP list's copy
     c.host_patch_dirty = std::max(c.host_patch_dirty, ndep);
     scatter_progressive(host, (const long long*)c.pin_pix, host_patch, ndep, ev[4]);
+    (void)hipGetLastError();   // a hipEventQuery's hipErrorNotReady is not a failure
     HIP_TRY(hipEventSynchronize(ev[4]));
     c.host_patch_dirty = 0;   // every entry below ndep consumed, none written above it
     if (g_e2e) {
