@@ -22,8 +22,14 @@ torch.distributed).
           ("strong").
   parity: the carry chain's resolver is serial, so the headline is N replicas,
           one image per GPU, no data-path collective ("weak"); the row-sharded single image
-          (rank 0 gathers the DEP entries, resolves, returns carry-ins) is timed after the
-          timed region and reported as `sharded_single_image` (--shard makes it the step).
+          (rank 0 receives the other ranks' DEP entries and row blocks, resolves the chain and
+          shades every DEP entry; nothing returns) is timed after the timed region and
+          reported as `sharded_single_image` (--shard makes it the step).
+
+What `value` includes is stated in the line itself (`config.timed_region`); `rates` puts the
+three rates side by side: frames in flight on the device (`value`), one frame at a time on the
+device (`single_frame`), and the drop-in raycast() call end to end — scene upload, kernels and
+the copy into the caller's fresh pageable pixmap (`end_to_end`, SURVEY.md §8d's rate).
 
 Rank 0 prints one JSON line with `roofline` (the dominant kernel, timed live with HIP events
 on its stream through rc_profile_begin/end), per-phase times and `cpu_baseline` (the reference
@@ -636,7 +642,16 @@ def main():
                        "parallelism": (f"row-cyclic shards x{world}, RCCL gather in the library "
                                        "(rc_render_sharded)" if sharded else
                                        (f"replicas x{world}" if world > 1 else "single GPU")),
-                       "frames_in_flight": 2 if piped else 1},
+                       "frames_in_flight": 2 if piped else 1,
+                       "timed_region": (
+                           ("device-resident: scene and output images in HBM, two parity frames "
+                            "in flight (rc_frame_submit), no scene upload and no copy to the host; "
+                            "the drop-in raycast() call (one image, upload + kernels + D2H into "
+                            "the caller's pixmap) is `end_to_end`") if piped else
+                           ("device-resident: one image per step, scene and output in HBM, no "
+                            "scene upload and no copy to the host"
+                            + ("; row-sharded over the group, gathered on rank 0" if sharded
+                               else "")))},
             "verified": verified,
             "phases_ms": {k: round(v, 4) for k, v in phases.items() if k.endswith("_ms")},
             "tuning": ({t.split("=", 1)[0]: int(t.split("=", 1)[1]) for t in args.tune}
@@ -694,6 +709,18 @@ def main():
                                    for k, v in shard_stats.items()}
         if world == 1 and not args.timed_only:
             line["end_to_end"] = end_to_end(pkg, scene, W, H, args.depth, mode)
+            rates = {"value_is": ("frames_in_flight_device" if piped else "one_frame_device"),
+                     "dropin_rate_is": "raycast_end_to_end (SURVEY.md §8d: upload + kernels + D2H)"}
+            if piped:
+                rates["frames_in_flight_device"] = {"value": round(value, 1),
+                                                    "ms_per_frame": round(step_ms, 4)}
+            if single:
+                rates["one_frame_device"] = {"value": single["value"], "ms": single["ms"]}
+            elif not piped and not sharded:
+                rates["one_frame_device"] = {"value": round(value, 1), "ms": round(step_ms, 4)}
+            rates["raycast_end_to_end"] = {"value": line["end_to_end"]["value"],
+                                           "ms": line["end_to_end"]["ms"]}
+            line["rates"] = rates
         if world == 1 and not args.no_cpu_baseline and not args.timed_only and mode != "cuda":
             line["cpu_baseline"] = cpu_baseline(scene_path, args.size, args.depth)
     # N>1 parity replicas: the sharded single image as well, reported beside (never as) value.

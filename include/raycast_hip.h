@@ -319,7 +319,9 @@ typedef struct rc_tuning {
                              runtime maps streams onto hardware queues in creation order): 0
                              lane by lane (resolver, phase C), then the pixel streams; 1
                              resolvers, pixel streams, phase C; 2 pixel streams, phase C,
-                             resolvers                                                        */
+                             resolvers; 3 each resolver lane on a hardware queue of its own
+                             (placeholder streams fill the others; needs two lanes and the
+                             default stream layout, else order 2 with a warning)          */
   int pipe_helpers;       /* frames in flight: dense-run helper workgroups per resolver lane
                              (default 4; 0 = none)                                            */
   int patch_host;         /* rc_render (parity, overlap_d2h): phase C writes the DEP entries'
@@ -328,6 +330,10 @@ typedef struct rc_tuning {
                              scatters each entry as it arrives, during the frame (default 2);
                              1: scattered after the frame; 0: a device buffer copied after
                              phase C                                                          */
+  int share_device;       /* rc_render / raycast() with num_gpus > 1: 0 one device per rank
+                             (devices device .. device+num_gpus-1, RCCL; fewer if the box has
+                             fewer, with a warning); 1 every rank on `device` with device
+                             copies between the ranks (the multi-GPU path on one GPU: tests) */
 } rc_tuning;
 void rc_default_tuning(rc_tuning *t);
 int rc_set_tuning(const rc_tuning *t);
@@ -337,9 +343,11 @@ void rc_get_tuning(rc_tuning *t);
  * Rows are dealt cyclically (image row y -> rank y % G).  Every rank renders its rows; the
  * root (rank 0) gathers the row blocks over RCCL (ncclGather over xGMI) and undoes the
  * interleave on its device.  Parity mode adds the carry chain's exchange: every rank runs
- * phase A on its rows, the root gathers the DEP entries (ncclSend/ncclRecv), resolves the
- * scan-order carry chain and sends each rank its carry-ins back for phase C.  The output is
- * byte-identical to rc_render on one device. */
+ * phase A on its rows, the root receives the other ranks' DEP entries and row blocks
+ * (ncclSend/ncclRecv; its own are read in place), rebuilds the scan-order DEP list, and its
+ * resolver resolves the carry chain and shades every DEP entry (phase C) straight into the
+ * image: nothing returns to the ranks.  The output is byte-identical to rc_render on one
+ * device. */
 #define RC_GROUP_ID_BYTES 128          /* == sizeof(ncclUniqueId) */
 enum { RC_XFER_AUTO = 0,   /* RCCL when every rank has its own device, else RC_XFER_COPY */
        RC_XFER_RCCL = 1,   /* RCCL communicators (xGMI)                                 */

@@ -117,7 +117,8 @@ TUNING_FIELDS = ["side", "split_shade", "resolve_shared", "resolve_lds_kb", "res
                  "pipe_resolvers", "pipe_slots", "pipe_timing", "pipe_slotstreams", "overlap_d2h",
                  "staged_d2h", "prefault", "copy_threads", "side_blocks", "comp_stream",
                  "block_min", "pipe_inres", "x0", "resolve_clean",
-                 "shard_lone", "team_cscan", "pipe_order", "pipe_helpers", "patch_host"]
+                 "shard_lone", "team_cscan", "pipe_order", "pipe_helpers", "patch_host",
+                 "share_device"]
 
 
 class RcTuning(ctypes.Structure):

@@ -78,6 +78,7 @@ rc_tuning default_tuning() {
   // 4.4 -> 2.5 ms, under the team segment); 8192^2 and pipeline lanes have more such segments
   // than workgroups and keep one wave per segment
   t.block_min = 3000;
+  t.share_device = 0;
   return t;
 }
 rc_tuning g_tune = default_tuning();
@@ -236,16 +237,23 @@ int ctx_get(int device, DevCtx** out) {
 // threads) and copies each chunk out with a small persistent thread pool.
 constexpr size_t kStageChunk = 8u << 20;
 
+// One pool per device: the in-frame scatter (scatter_progressive) keeps a device's pool busy
+// for most of its frame, and rc_render callers on other devices must not wait for that.
 class HostPool {
  public:
-  static HostPool& get() {   // never destroyed: its detached workers outlive main()
-    static HostPool* pool = new HostPool();
-    return *pool;
+  static HostPool& get(int device) {   // never destroyed: its detached workers outlive main()
+    static std::mutex mu;
+    static HostPool* pools[kMaxDevices] = {};
+    const int d = device >= 0 && device < kMaxDevices ? device : 0;
+    std::lock_guard<std::mutex> lk(mu);
+    if (!pools[d]) pools[d] = new HostPool();
+    return *pools[d];
   }
   int parts() const { return nthreads_ + 1; }
-  // fn(part, parts) on the workers and the calling thread (part 0), one call at a time
+  // fn(part, parts) on the workers and the calling thread (part 0), one call at a time (the
+  // device's callers already hold its lock; this also orders calls that do not)
   void run(const std::function<void(int, int)>& fn) {
-    std::lock_guard<std::mutex> one_at_a_time(call_mu_);   // rc_render callers on other devices
+    std::lock_guard<std::mutex> one_at_a_time(call_mu_);
     {
       std::unique_lock<std::mutex> lk(mu_);
       fn_ = &fn;
@@ -268,8 +276,14 @@ class HostPool {
 
  private:
   HostPool() {
-    g_pool_threads = tune().copy_threads;
-    int t = tune().copy_threads - 1;
+    // every device's pool has the size the first one was built with (rc_set_tuning warns)
+    int want = g_pool_threads.load();
+    if (want < 0) {
+      want = tune().copy_threads;
+      int expect = -1;
+      if (!g_pool_threads.compare_exchange_strong(expect, want)) want = expect;
+    }
+    int t = want - 1;
     if (t < 0) t = 0;
     if (t > 31) t = 31;
     nthreads_ = t;
@@ -300,8 +314,9 @@ class HostPool {
   const std::function<void(int, int)>* fn_ = nullptr;
 };
 
-int copy_to_host(DevCtx& c, uint8_t* host, const uint8_t* dev, size_t bytes, hipStream_t st) {
-  if (!tune().staged_d2h) {   // the runtime's pageable copy
+int copy_to_host(DevCtx& c, uint8_t* host, const uint8_t* dev, size_t bytes, hipStream_t st,
+                 const rc_tuning& tu) {
+  if (!tu.staged_d2h) {   // the runtime's pageable copy
     HIP_TRY(hipMemcpyAsync(host, dev, bytes, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     return 0;
@@ -322,7 +337,7 @@ int copy_to_host(DevCtx& c, uint8_t* host, const uint8_t* dev, size_t bytes, hip
   for (size_t i = 0; i < n; ++i) {
     const int b = (int)(i & 1);
     HIP_TRY(hipEventSynchronize(c.stage_ev[b]));
-    HostPool::get().copy(host + i * kStageChunk, c.stage[b], chunk(i));
+    HostPool::get(c.device).copy(host + i * kStageChunk, c.stage[b], chunk(i));
     if (i + 2 < n) {
       HIP_TRY(hipMemcpyAsync(c.stage[b], dev + (i + 2) * kStageChunk, chunk(i + 2),
                              hipMemcpyDeviceToHost, st));
@@ -334,9 +349,9 @@ int copy_to_host(DevCtx& c, uint8_t* host, const uint8_t* dev, size_t bytes, hip
 
 // Fault the caller's fresh pixmap in (C/raycast.c:52-53 mallocs it) over the host pool while the
 // GPU renders, instead of inside the copy (every byte is overwritten afterwards).
-void prefault(uint8_t* p, size_t n) {
-  if (!n || !tune().prefault) return;
-  HostPool::get().run([&](int part, int parts) {
+void prefault(DevCtx& c, uint8_t* p, size_t n, const rc_tuning& tu) {
+  if (!n || !tu.prefault) return;
+  HostPool::get(c.device).run([&](int part, int parts) {
     const size_t per = ((n + parts - 1) / parts + 4095) & ~(size_t)4095;
     const size_t a = (size_t)part * per, b = a + per < n ? a + per : n;
     volatile uint8_t* q = p;
@@ -363,9 +378,12 @@ int ensure_pinned(DevCtx& c, size_t entries) {
 // of an 11 MB copy (quadric 4096^2) after the frame's last kernel.  Entries carry a ready mark
 // (kPatchReady), so for patch_host 2 the array must start the frame cleared: that scatter clears
 // what it consumes; patch_host 1's (and a frame that ended early) leave host_patch_dirty entries.
-int ensure_host_patch(DevCtx& c, size_t entries) {
+// rc_render raises host_patch_dirty to the whole image before it enqueues a frame that writes
+// the array and lowers it to the frame's DEP count once that is known, so a frame that fails
+// before then still has its marks cleared.
+int ensure_host_patch(DevCtx& c, size_t entries, int patch_host) {
   if (entries <= c.host_patch_entries) {
-    if (tune().patch_host == 2 && c.host_patch_dirty) {
+    if (patch_host == 2 && c.host_patch_dirty) {
       std::memset(c.host_patch, 0, c.host_patch_dirty * sizeof(uint32_t));
       c.host_patch_dirty = 0;
     }
@@ -389,17 +407,21 @@ int ensure_host_patch(DevCtx& c, size_t entries) {
 // thread sweeps its share of the DEP list, scatters every entry phase C has marked ready and
 // clears it, until its share is done; once the frame's last kernel has completed (ev_done),
 // one more sweep takes everything left.  The framebuffer copy must already be in `host` (it
-// carries the DEP pixels' phase-A bytes, which the patch overwrites).
-void scatter_progressive(uint8_t* host, const long long* pix, uint32_t* patch, size_t ndep,
-                         hipEvent_t ev_done) {
+// carries the DEP pixels' phase-A bytes, which the patch overwrites).  A sweep that found
+// nothing yields before the next; any event status other than "not ready" ends every thread's
+// sweeps (the frame failed: returns -1, the caller reports it).
+int scatter_progressive(DevCtx& c, uint8_t* host, const long long* pix, uint32_t* patch,
+                        size_t ndep, hipEvent_t ev_done) {
   std::atomic<bool> over{false};
-  HostPool::get().run([&](int part, int parts) {
+  std::atomic<int> status{(int)hipSuccess};
+  HostPool::get(c.device).run([&](int part, int parts) {
     const size_t per = (ndep + parts - 1) / parts;
     const size_t a = (size_t)part * per, b = a + per < ndep ? a + per : ndep;
     if (a >= b) return;
     size_t left = b - a, lo = a;   // lo: entries below it are all consumed
     for (;;) {
       const bool last = over.load(std::memory_order_acquire);
+      if (status.load(std::memory_order_relaxed) != (int)hipSuccess) return;
       size_t got = 0;
       bool gap = false;
       for (size_t j = lo; j < b; ++j) {
@@ -419,9 +441,29 @@ void scatter_progressive(uint8_t* host, const long long* pix, uint32_t* patch, s
       }
       left -= got;
       if (!left || last) return;   // after the frame an unmarked entry stays unmarked
-      if (!got && hipEventQuery(ev_done) == hipSuccess) over.store(true, std::memory_order_release);
+      if (!got) {
+        const hipError_t q = hipEventQuery(ev_done);
+        if (q == hipSuccess) {
+          over.store(true, std::memory_order_release);
+        } else if (q != hipErrorNotReady) {
+          status.store((int)q, std::memory_order_relaxed);
+          return;
+        } else {
+          std::this_thread::yield();
+        }
+      }
     }
   });
+  // a query's hipErrorNotReady is not a failure: clear it from this thread's last error (the
+  // pool's threads keep theirs; nothing reads them)
+  (void)hipGetLastError();
+  const int st = status.load();
+  if (st != (int)hipSuccess) {
+    std::fprintf(stderr, "Error: HIP call failed: hipEventQuery (%s) during the in-frame scatter\n",
+                 hipGetErrorString((hipError_t)st));
+    return -1;
+  }
+  return 0;
 }
 
 // RC_E2E_TRACE=1: rc_render prints its host-side marks (ms from entry) to stderr, to split the
@@ -444,7 +486,9 @@ struct E2eTrace {
                    at[0], at[1], at[2], at[3], at[4], at[5], at[6], at[7]);
   }
 };
-E2eTrace* g_e2e = nullptr;   // set for the duration of one traced rc_render (under c->mu)
+// set for the duration of one traced rc_render, on its own thread (renders on other devices
+// run concurrently)
+thread_local E2eTrace* g_e2e = nullptr;
 
 // The parity render's device-to-host copy, overlapped with the render (the
 // drop-in rate spans upload + kernels + copy).  Once phase A and the compaction are done
@@ -454,8 +498,12 @@ E2eTrace* g_e2e = nullptr;   // set for the duration of one traced rc_render (un
 // pixels), and the host pool scatters them over the copy — or, with patch_host, phase C wrote
 // them into mapped host memory and the pool scatters each as it arrives (scatter_progressive),
 // so only the frame's last entries are left once it ends.
+// host_patch: the mapped array phase C writes (patch_host 1 or 2, tu.patch_host says which);
+// prev_dirty: its entries an earlier frame may have left marked (rc_render has raised
+// host_patch_dirty to the whole image for this frame; it drops to the frame's own bound here).
 int copy_overlapped(DevCtx& c, uint8_t* host, const uint8_t* dev, size_t bytes,
-                    const hipEvent_t* ev, uint32_t* host_patch) {
+                    const hipEvent_t* ev, uint32_t* host_patch, size_t prev_dirty,
+                    const rc_tuning& tu) {
   if (ensure_pinned(c, 0)) return -1;
   HIP_TRY(hipEventSynchronize(ev[2]));
   if (g_e2e) g_e2e->mark(2);
@@ -463,19 +511,22 @@ int copy_overlapped(DevCtx& c, uint8_t* host, const uint8_t* dev, size_t bytes,
                          c.d2h));
   HIP_TRY(hipStreamSynchronize(c.d2h));
   const size_t ndep = (size_t)c.pin_cnt[2];
+  // the frame writes (and marks) only entries below its DEP count
+  if (host_patch) c.host_patch_dirty = std::max(prev_dirty, ndep);
   if (ensure_pinned(c, ndep)) return -1;
   if (ndep)
     HIP_TRY(hipMemcpyAsync(c.pin_pix, c.fb.dep_pix.p, ndep * sizeof(long long),
                            hipMemcpyDeviceToHost, c.d2h));
-  if (copy_to_host(c, host, dev, bytes, c.d2h)) return -1;
+  if (copy_to_host(c, host, dev, bytes, c.d2h, tu)) return -1;
   if (g_e2e) g_e2e->mark(3);
-  if (host_patch && ndep && tune().patch_host == 2) {   // consumed as it arrives
+  if (host_patch && ndep && tu.patch_host == 2) {   // consumed as it arrives
     HIP_TRY(hipStreamSynchronize(c.d2h));   // the DEP list's copy
-    c.host_patch_dirty = std::max(c.host_patch_dirty, ndep);
-    scatter_progressive(host, (const long long*)c.pin_pix, host_patch, ndep, ev[4]);
-    (void)hipGetLastError();   // a hipEventQuery's hipErrorNotReady is not a failure
+    if (scatter_progressive(c, host, (const long long*)c.pin_pix, host_patch, ndep, ev[4]))
+      return -1;
     HIP_TRY(hipEventSynchronize(ev[4]));
-    c.host_patch_dirty = 0;   // every entry below ndep consumed, none written above it
+    // every entry below ndep consumed and cleared, none written above it; entries an earlier
+    // frame left marked were cleared before this frame (ensure_host_patch)
+    c.host_patch_dirty = 0;
     if (g_e2e) {
       g_e2e->mark(4);
       g_e2e->mark(5);
@@ -487,7 +538,6 @@ int copy_overlapped(DevCtx& c, uint8_t* host, const uint8_t* dev, size_t bytes,
   if (!ndep) return 0;
   const uint32_t* rgb = host_patch;   // written by phase C itself (patch_host 1)
   if (rgb) {
-    c.host_patch_dirty = std::max(c.host_patch_dirty, ndep);   // its ready marks stay
     HIP_TRY(hipStreamSynchronize(c.d2h));   // the DEP list's copy
   } else {
     HIP_TRY(hipMemcpyAsync(c.pin_patch, c.patch.p, ndep * sizeof(uint32_t),
@@ -496,7 +546,7 @@ int copy_overlapped(DevCtx& c, uint8_t* host, const uint8_t* dev, size_t bytes,
     rgb = (const uint32_t*)c.pin_patch;
   }
   const long long* pix = (const long long*)c.pin_pix;
-  HostPool::get().run([&](int part, int parts) {
+  HostPool::get(c.device).run([&](int part, int parts) {
     const size_t per = (ndep + parts - 1) / parts;
     const size_t a = (size_t)part * per, b = a + per < ndep ? a + per : ndep;
     for (size_t j = a; j < b; ++j) {
@@ -545,7 +595,7 @@ int rc_set_tuning(const rc_tuning* t) {
       in(t->block_min, 0, 1 << 30) && in(t->pipe_inres, 0, 2) && in(t->x0, 0, 1) &&
       in(t->resolve_clean, 1, 64) && in(t->shard_lone, 0, 1) && in(t->team_cscan, 0, 1) &&
       in(t->pipe_order, 0, 3) && in(t->pipe_helpers, 0, rc::kDenseSlots) &&
-      in(t->patch_host, 0, 2) &&
+      in(t->patch_host, 0, 2) && in(t->share_device, 0, 1) &&
       !(t->split_shade && !t->side);
   if (!ok) {
     std::fprintf(stderr, "Error: rc_set_tuning: a field is out of range\n");
@@ -1278,6 +1328,10 @@ int pipe_init(DevCtx& c, long long pixels) {
     HIP_TRY(hipExtStreamCreateWithCUMask(&p.pix[1], (uint32_t)words, mb.data()));
     HIP_TRY(hipExtStreamCreateWithCUMask(&p.pc[1], (uint32_t)words, mb.data()));
   } else {
+    if (tu.pipe_order == 3)
+      std::fprintf(stderr, "Warning: pipe_order 3 needs two resolver lanes and the default "
+                   "stream layout (pipe_resolvers %d, pipe_slotstreams %d): using order 2\n",
+                   p.lanes, p.fifo ? 0 : 1);
     if (mk_pix() || mk_pc() || mk_res()) return -1;
   }
   for (int k = 0; k < p.slots; ++k) {
@@ -1547,6 +1601,8 @@ int rc_render(const rc_scene* s, int W, int H, const rc_options* opt, uint8_t* p
   if (!s || !opt || !pixmap || W <= 0 || H <= 0) return -1;
   auto t0 = std::chrono::steady_clock::now();
   if (timing) std::memset(timing, 0, sizeof *timing);
+  // one snapshot of the tuning for the whole call (rc_set_tuning may run concurrently)
+  const rc_tuning tu = tune();
   int ndev = 0;
   HIP_TRY(hipGetDeviceCount(&ndev));
   int G = opt->num_gpus;
@@ -1554,9 +1610,21 @@ int rc_render(const rc_scene* s, int W, int H, const rc_options* opt, uint8_t* p
     std::fprintf(stderr, "Error: device %d not available (%d devices)\n", opt->device, ndev);
     return -1;
   }
-  if (G > ndev - opt->device) G = ndev - opt->device;
-  if (G > rc::kMaxShards) G = rc::kMaxShards;
-  if (G > H) G = H;
+  // share_device: every rank on opt->device (device copies between the ranks: tests of the
+  // multi-GPU entry on a one-GPU box); otherwise one device per rank
+  const int avail = tu.share_device ? rc::kMaxShards : ndev - opt->device;
+  if (G > avail || G > rc::kMaxShards || G > H) {
+    const int want = G;
+    if (G > avail) G = avail;
+    if (G > rc::kMaxShards) G = rc::kMaxShards;
+    if (G > H) G = H;
+    static std::atomic<bool> warned{false};   // once per process, like the reference's notices
+    if (!warned.exchange(true))
+      std::fprintf(stderr,
+                   "Warning: %d GPUs requested (RAYCAST_GPUS / num_gpus); rendering on %d (%d "
+                   "devices from device %d, at most %d shards, %d rows)\n",
+                   want, G, ndev - opt->device, opt->device, rc::kMaxShards, H);
+  }
   const bool parity = opt->mode == RC_MODE_PARITY && opt->max_recursion > 1;
   const size_t row_bytes = (size_t)W * 3;
   if (G > 1) {   // row shards over RCCL (rc_shard.hip), the image on the first device
@@ -1566,13 +1634,14 @@ int rc_render(const rc_scene* s, int W, int H, const rc_options* opt, uint8_t* p
     std::lock_guard<std::mutex> one_group_call(group_call_mu);
     uint8_t* d_image = nullptr;
     rc_timing tg;
-    if (render_local_group(opt->device, G, s, W, H, opt, &d_image, &tg)) return -1;
+    if (render_local_group(opt->device, G, tu.share_device != 0, s, W, H, opt, &d_image, &tg))
+      return -1;
     DevCtx* c;
     if (hipSetDevice(opt->device) != hipSuccess || ctx_get(opt->device, &c)) return -1;
     std::lock_guard<std::mutex> lk(c->mu);
-    prefault(pixmap, (size_t)H * row_bytes);
+    prefault(*c, pixmap, (size_t)H * row_bytes, tu);
     auto td = std::chrono::steady_clock::now();
-    if (copy_to_host(*c, pixmap, d_image, (size_t)H * row_bytes, c->stream)) return -1;
+    if (copy_to_host(*c, pixmap, d_image, (size_t)H * row_bytes, c->stream, tu)) return -1;
     if (timing) {
       *timing = tg;
       timing->d2h_ms =
@@ -1600,14 +1669,18 @@ int rc_render(const rc_scene* s, int W, int H, const rc_options* opt, uint8_t* p
   uint8_t* d_out = (uint8_t*)c->out.p;
   // parity: the copy overlaps the resolver (copy_overlapped); split shading leaves the non-DEP
   // colours to phase C, so its framebuffer is not final after phase A
-  const bool overlap = parity && !tune().split_shade && tune().overlap_d2h;
+  const bool overlap = parity && !tu.split_shade && tu.overlap_d2h;
   uint32_t* patch = nullptr;
-  const bool hpatch = overlap && tune().patch_host;
+  const bool hpatch = overlap && tu.patch_host;
+  size_t prev_dirty = 0;
   if (overlap) {
     if (!c->d2h && hipStreamCreateWithFlags(&c->d2h, hipStreamNonBlocking) != hipSuccess) return -1;
     if (hpatch) {
-      if (ensure_host_patch(*c, (size_t)W * H)) return -1;
+      if (ensure_host_patch(*c, (size_t)W * H, tu.patch_host)) return -1;
       patch = c->host_patch_dev;
+      // until the frame's DEP count is known (copy_overlapped), any entry may get a mark
+      prev_dirty = c->host_patch_dirty;
+      c->host_patch_dirty = (size_t)W * H;
     } else {
       if (c->patch.ensure((size_t)W * H * sizeof(uint32_t))) return -1;
       patch = (uint32_t*)c->patch.p;
@@ -1623,14 +1696,14 @@ int rc_render(const rc_scene* s, int W, int H, const rc_options* opt, uint8_t* p
   if (E2eTrace::on()) g_e2e = &trace;
   if (enqueue_render(*c, s, W, H, 0, 1, H, opt, d_out, c->stream, true, patch, &ev)) return -1;
   trace.mark(0);
-  prefault(pixmap, (size_t)H * row_bytes);
+  prefault(*c, pixmap, (size_t)H * row_bytes, tu);
   trace.mark(1);
   auto td = std::chrono::steady_clock::now();
   if (overlap) {
     if (copy_overlapped(*c, pixmap, d_out, (size_t)H * row_bytes, ev,
-                        hpatch ? c->host_patch : nullptr))
+                        hpatch ? c->host_patch : nullptr, prev_dirty, tu))
       return -1;
-  } else if (copy_to_host(*c, pixmap, d_out, (size_t)H * row_bytes, c->stream)) {
+  } else if (copy_to_host(*c, pixmap, d_out, (size_t)H * row_bytes, c->stream, tu)) {
     return -1;
   }
   // this frame's latched hand-off words: its own failure is reported by this call and

@@ -215,9 +215,11 @@ rc_tuning tune();
 int ctx_get(int device, DevCtx** out);
 int fill_resolver_stats(DevCtx& c, const FrameLog::Diag& d, int grid, int res_cus, int lds,
                         int team, rc_resolver_stats* r);
-int copy_to_host(DevCtx& c, uint8_t* host, const uint8_t* dev, size_t bytes, hipStream_t st);
-int ensure_host_patch(DevCtx& c, size_t entries);
-void prefault(uint8_t* p, size_t n);
+// the host-side copy helpers take the caller's one tuning snapshot (rc_render)
+int copy_to_host(DevCtx& c, uint8_t* host, const uint8_t* dev, size_t bytes, hipStream_t st,
+                 const rc_tuning& tu);
+int ensure_host_patch(DevCtx& c, size_t entries, int patch_host);
+void prefault(DevCtx& c, uint8_t* p, size_t n, const rc_tuning& tu);
 int upload_scene(FrameBufs& b, hipStream_t stream, const rc_scene* s, rc::LaunchScene& ls);
 int ensure_parity(DevCtx& c, FrameBufs& b, int W, int H, rc::ParityWork& w, int res_cus,
                   int piped_lane = -1);
@@ -231,9 +233,10 @@ int enqueue_render(DevCtx& c, const rc_scene* s, int W, int H, int row0, int row
 int check_spin_error(FrameBufs& b, const rc_options* opt);
 void fill_device_timing(DevCtx& c, const rc_options* opt, rc_timing* t);
 // rc_shard.hip: rc_render's multi-GPU path (a cached in-process group over devices
-// first..first+n-1); *d_image = the root's de-interleaved image.  The caller holds no lock.
-int render_local_group(int first, int n, const rc_scene* s, int W, int H, const rc_options* opt,
-                       uint8_t** d_image, rc_timing* timing);
+// first..first+n-1, or n ranks sharing device `first` with device copies between them when
+// `share`); *d_image = the root's de-interleaved image.  The caller holds no lock.
+int render_local_group(int first, int n, bool share, const rc_scene* s, int W, int H,
+                       const rc_options* opt, uint8_t** d_image, rc_timing* timing);
 
 }  // namespace rcrt
 

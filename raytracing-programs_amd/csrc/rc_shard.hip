@@ -589,7 +589,8 @@ int render_sharded(rc_group& g, const rc_scene* s, int W, int H, const rc_option
       st.phase_c_ms = event_ms(root->ev[3], root->ev[4]);
       st.image_ms = event_ms(root->ev[4], root->ev[5]);
       for (int q = 0; q < G; ++q) st.dep_pixels += root->h_small_all[4 * q];
-      st.entry_bytes = st.dep_pixels * (long long)rc::shard_entry_bytes();
+      // what moved: the other ranks' wire records (the root's own entries are read in place)
+      st.entry_bytes = (st.dep_pixels - root->h_small_all[0]) * (long long)rc::shard_entry_bytes();
       st.carry_bytes = 0;
     } else {
       st.image_ms = event_ms(root->ev[1], root->ev[5]);
@@ -629,21 +630,25 @@ struct DeviceLocks {
 
 namespace rcrt {
 
-// rc_render's multi-GPU path: a cached in-process group over devices first..first+n-1.
-int render_local_group(int first, int n, const rc_scene* s, int W, int H, const rc_options* opt,
-                       uint8_t** d_image, rc_timing* timing) {
+// rc_render's multi-GPU path: a cached in-process group over devices first..first+n-1 (RCCL),
+// or n ranks on device `first` (share: device copies, rc_tuning.share_device).
+int render_local_group(int first, int n, bool share, const rc_scene* s, int W, int H,
+                       const rc_options* opt, uint8_t** d_image, rc_timing* timing) {
   static std::mutex mu;
   static rc_group* cached = nullptr;
   static int c_first = -1, c_n = 0;
+  static bool c_share = false;
   std::lock_guard<std::mutex> lk(mu);
-  if (!cached || c_first != first || c_n != n) {
+  if (!cached || c_first != first || c_n != n || c_share != share) {
     if (cached) rc_group_destroy(cached);
+    cached = nullptr;
     std::vector<int> devs(n);
-    for (int i = 0; i < n; ++i) devs[i] = first + i;
-    cached = rc_group_create_local(n, devs.data(), RC_XFER_AUTO);
+    for (int i = 0; i < n; ++i) devs[i] = share ? first : first + i;
+    cached = rc_group_create_local(n, devs.data(), share ? RC_XFER_COPY : RC_XFER_AUTO);
     if (!cached) return -1;
     c_first = first;
     c_n = n;
+    c_share = share;
   }
   DeviceLocks locks(*cached);
   if (render_sharded_retry(*cached, s, W, H, opt, nullptr, timing)) return -1;

@@ -137,10 +137,10 @@ def test_sharded_rccl_one_rank(mode, scenes, table):
 def test_sharded_rccl_one_rank_exchange(mode, scenes, table):
     """One-rank RCCL groups through the sharded exchange instead of the lone-frame bypass
     (rc_tuning.shard_lone = 0), on both group kinds: the row-block ncclGather, and in parity the
-    exact-size exchange of a new key (ncclSend/ncclRecv), the fixed-size one of repeated frames
-    (ncclGather / ncclScatter of padded blocks), the ncclAllReduce of the entry counts that
-    bounds the next frame, and an overflowed bound (rendered again exactly).  Every image
-    md5-equal to the reference."""
+    exact-size exchange of a new key and the fixed-size one of repeated frames (both
+    ncclSend/ncclRecv; the fixed-size one with padded per-rank blocks), the ncclAllReduce of the
+    entry counts that bounds the next frame, and an overflowed bound (rendered again exactly).
+    Every image md5-equal to the reference."""
     key = "quadric:1024x1024:d6:" + mode
     want = table[key]["md5"]
     with rc.tuned(shard_lone=0):
@@ -166,17 +166,19 @@ def test_sharded_rccl_one_rank_exchange(mode, scenes, table):
 
 def test_sharded_repeat_and_stats(scenes, table):
     """Back-to-back sharded frames reuse every buffer (carry-in tags advance per frame); the
-    exchange volumes follow the wire format (80 B per DEP entry in, nothing back: phase C runs
-    on the root); every rank's own timeline is recorded (rc_group_rank_stats)."""
+    exchange volumes follow the wire format (80 B per DEP entry of the other ranks in — the
+    root's own entries are read in place — and nothing back: phase C runs on the root); every
+    rank's own timeline is recorded (rc_group_rank_stats)."""
     key = "quadric:4096x4096:d6:parity"
     g4 = group([0] * 4, "copy")
     for _ in range(3):
         assert p3_md5(sharded(g4, scenes["quadric"], 4096, 4096, 6, "parity")) == table[key]["md5"]
     st = g4.stats()
     assert st["ranks"] == 4 and st["dep_pixels"] == 2804464
-    assert st["entry_bytes"] == 80 * st["dep_pixels"] and st["carry_bytes"] == 0
-    assert st["resolve_ms"] > 0.0 and st["device_ms"] >= st["resolve_ms"]
     ranks = [g4.rank_stats(r) for r in range(4)]
+    assert st["entry_bytes"] == 80 * (st["dep_pixels"] - ranks[0]["dep_pixels"])
+    assert st["carry_bytes"] == 0
+    assert st["resolve_ms"] > 0.0 and st["device_ms"] >= st["resolve_ms"]
     assert [q["rank"] for q in ranks] == [0, 1, 2, 3] and sum(q["rows"] for q in ranks) == 4096
     assert sum(q["dep_pixels"] for q in ranks) == st["dep_pixels"]
     assert all(q["local_ms"] > 0.0 and q["total_ms"] >= q["local_ms"] for q in ranks)
@@ -211,3 +213,30 @@ def test_sharded_fixed_exchange(G, scenes, table):
     assert p3_md5(sharded(g, scenes["quadric"], 1024, 1024, 6, "parity")) == want, "overflow"
     assert p3_md5(sharded(g, scenes["quadric"], 1024, 1024, 6, "parity")) == want, "after"
     g.debug_bound(-1)
+
+
+@pytest.mark.parametrize("mode", ["parity", "fast"])
+@pytest.mark.parametrize("G", [2, 8])
+def test_render_num_gpus_shared_device(G, mode, scenes, table):
+    """The drop-in's multi-GPU entry — rc_render (raycast()'s path, RAYCAST_GPUS) with num_gpus
+    > 1 — through its cached local group, here with every rank on device 0
+    (rc_tuning.share_device: device copies between the ranks) at C4, md5 vs the reference."""
+    key = "quadric:4096x4096:d6:" + mode
+    with rc.tuned(share_device=1):
+        for _ in range(2):   # the group is built once, then reused
+            t = {}
+            img = rc.render(scenes["quadric"], 4096, 4096, depth=6, mode=mode, gpus=G, timing=t)
+            assert p3_md5(img) == table[key]["md5"], f"G={G}"
+            if mode == "parity":
+                assert t["dep_pixels"] == 2804464
+
+
+def test_render_num_gpus_clamped_warns(scenes, table, capfd):
+    """More GPUs than the box has (one here, unless the box is bigger): rc_render renders on
+    the devices there are and says so on stderr (once per process), md5 unchanged."""
+    ndev = torch.cuda.device_count()
+    key = "quadric:256x256:d6:parity"
+    img = rc.render(scenes["quadric"], 256, 256, depth=6, gpus=ndev + 3)
+    assert p3_md5(img) == table[key]["md5"]
+    err = capfd.readouterr().err
+    assert f"{ndev + 3} GPUs requested" in err and f"rendering on {ndev}" in err
