@@ -334,6 +334,9 @@ typedef struct rc_tuning {
                              (devices device .. device+num_gpus-1, RCCL; fewer if the box has
                              fewer, with a warning); 1 every rank on `device` with device
                              copies between the ranks (the multi-GPU path on one GPU: tests) */
+  int headb_first;        /* one frame at a time: resolver workgroups that skip the whole-
+                             workgroup queue of long regular segments and start at once on the
+                             per-wave queue, whose front holds the runs that can be dense    */
 } rc_tuning;
 void rc_default_tuning(rc_tuning *t);
 int rc_set_tuning(const rc_tuning *t);

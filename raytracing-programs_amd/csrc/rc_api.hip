@@ -79,6 +79,10 @@ rc_tuning default_tuning() {
   // than workgroups and keep one wave per segment
   t.block_min = 3000;
   t.share_device = 0;
+  // round 5: 24 of the lone resolver's regular workgroups start on the per-wave queue at once,
+  // so the dense runs reach the helpers ~0.5 ms earlier and the team segment alone bounds the
+  // resolver (lone quadric 4096^2 4.66 -> 4.55-4.56 ms; profiles/r05e_lone_headb.txt)
+  t.headb_first = 24;
   return t;
 }
 rc_tuning g_tune = default_tuning();
@@ -595,7 +599,7 @@ int rc_set_tuning(const rc_tuning* t) {
       in(t->block_min, 0, 1 << 30) && in(t->pipe_inres, 0, 2) && in(t->x0, 0, 1) &&
       in(t->resolve_clean, 1, 64) && in(t->shard_lone, 0, 1) && in(t->team_cscan, 0, 1) &&
       in(t->pipe_order, 0, 3) && in(t->pipe_helpers, 0, rc::kDenseSlots) &&
-      in(t->patch_host, 0, 2) && in(t->share_device, 0, 1) &&
+      in(t->patch_host, 0, 2) && in(t->share_device, 0, 1) && in(t->headb_first, 0, 1 << 16) &&
       !(t->split_shade && !t->side);
   if (!ok) {
     std::fprintf(stderr, "Error: rc_set_tuning: a field is out of range\n");
@@ -859,6 +863,10 @@ int ensure_parity(DevCtx& c, FrameBufs& b, int W, int H, rc::ParityWork& w, int 
   w.hand_run = tu.hand_run;
   w.long_len = tu.long_len;
   w.block_min = tu.block_min;
+  w.headb_first = piped ? 0 : tu.headb_first;
+  if (w.headb_first > w.resolve_blocks - w.team_blocks - w.helpers)
+    w.headb_first = w.resolve_blocks - w.team_blocks - w.helpers;
+  if (w.headb_first < 0) w.headb_first = 0;
   w.wave_k = tu.wave_k;
   w.resolve_k = tu.resolve_k;
   w.resolve_clean = tu.resolve_clean;

@@ -78,6 +78,7 @@ struct ParityWork {
   int inres;                // phase C inside the resolver: its waves shade ready batches once
                             // their own work is done (rc_tuning.side 3)
   int block_min;            // regular segments of >= block_min entries get a whole workgroup
+  int headb_first;          // regular workgroups that start on the per-wave queue (head B) at once
 };
 
 constexpr int kSegOrderMax = 65536;   // segments ordered for the resolver queue (else FIFO)

@@ -1862,7 +1862,8 @@ __global__ void __launch_bounds__(kResolveBlock) __attribute__((amdgpu_waves_per
     CinG* __restrict__ cin, int team_blocks, int long_len, TeamState* __restrict__ ts,
     unsigned* __restrict__ trace, int G, int wave_k, int resolve_k, int resolve_clean,
     int team_cscan, unsigned tag,
-    int helpers, int hand_run, int inject, int block_min, int* __restrict__ rq_cnt,
+    int helpers, int hand_run, int inject, int block_min, int headb_first,
+    int* __restrict__ rq_cnt,
     int* __restrict__ rq, Cam cam, int W, uint8_t* __restrict__ out, uint32_t* __restrict__ patch,
     unsigned long long* __restrict__ zcount, int* __restrict__ batch_state, int inres) {
   if (!RC_X0_RESOLVE) sc.has_quadric = sc.has_quadric != 0;   // no cross-term-free form here (RC_X0_*)
@@ -2341,7 +2342,10 @@ __global__ void __launch_bounds__(kResolveBlock) __attribute__((amdgpu_waves_per
   // held back behind the long ones, and take what is left of head A at the end.
   const int nlong = counters[14];
   int* headb = counters + 15;
-  if (nlong > 0 && (int)blockIdx.x >= team_blocks + helpers) {
+  // the first headb_first regular workgroups leave head A to the others and start on head B at
+  // once: its front holds the shorter segments that can turn out to be dense runs (every entry
+  // a changer), which a helper then takes after hand_run changes
+  if (nlong > 0 && (int)blockIdx.x >= team_blocks + helpers + headb_first) {
     __shared__ int s_seg;
     const int t = threadIdx.x;
     for (;;) {
@@ -2985,7 +2989,7 @@ hipError_t launch_parity(const LaunchScene& s, int W, int H, int maxrec, uint8_t
                      w.seg_key);
   hipLaunchKernelGGL(k_seg_order, dim3(1), dim3(1024), 0, stream, w.seg_start, w.counters,
                      w.seg_order, w.batch_state, w.batch_cnt, w.batch_rq, w.block_min,
-                     w.resolve_blocks - w.team_blocks - w.helpers, w.batch_ints > 0 ? 0 : 1);
+                     w.resolve_blocks - w.team_blocks - w.helpers - w.headb_first, w.batch_ints > 0 ? 0 : 1);
   // resolve_lds > 80 KiB keeps one resolver block (4 waves, one per SIMD) per CU: the chain
   // steps are latency-bound, so a resolver wave should not share its SIMD
   if (ev) (void)hipEventRecord(ev[1], stream);
@@ -3003,7 +3007,7 @@ hipError_t launch_parity(const LaunchScene& s, int W, int H, int maxrec, uint8_t
                      w.seg_start, w.seg_order, w.counters, w.counters + 1, (CinG*)w.cin, w.team_blocks,
                      w.long_len, (TeamState*)w.team, w.trace, w.coop_group, w.wave_k,
                      w.resolve_k, w.resolve_clean > 0 ? w.resolve_clean : 1, w.team_cscan, w.epoch, w.helpers, w.hand_run, w.inject, w.block_min,
-                     (w.side || w.inres) ? w.batch_cnt : nullptr, w.batch_rq, cam, W, out,
+                     w.headb_first, (w.side || w.inres) ? w.batch_cnt : nullptr, w.batch_rq, cam, W, out,
                      w.patch, zcount, w.batch_state, w.inres);
   if (w.rstream) {
     if (w.rt1) (void)hipEventRecord(w.rt1, rs);
@@ -3188,7 +3192,7 @@ hipError_t launch_shard_resolve(const LaunchScene& s, int W, int H, int G, int r
                      w.seg_key, w.wcarry, bound, thin0);
   hipLaunchKernelGGL(k_seg_order, dim3(1), dim3(1024), 0, stream, w.seg_start, w.counters,
                      w.seg_order, w.batch_state, w.batch_cnt, w.batch_rq, w.block_min,
-                     w.resolve_blocks - w.team_blocks - w.helpers, 1);
+                     w.resolve_blocks - w.team_blocks - w.helpers - w.headb_first, 1);
   if (ev) (void)hipEventRecord(ev[0], stream);
   // a lone frame's resolver from here on: phase C inside it (w.inres) shades every DEP entry
   // of the image into `out` — the root's image, whose non-DEP pixels the gathered row blocks
@@ -3200,7 +3204,7 @@ hipError_t launch_shard_resolve(const LaunchScene& s, int W, int H, int G, int r
                      w.team_blocks, w.long_len, (TeamState*)w.team, w.trace, w.coop_group,
                      w.wave_k, w.resolve_k, w.resolve_clean > 0 ? w.resolve_clean : 1,
                      w.team_cscan, w.epoch, w.helpers, w.hand_run, w.inject, w.block_min,
-                     w.inres ? w.batch_cnt : nullptr, w.batch_rq, cam, W, out, (uint32_t*)nullptr,
+                     w.headb_first, w.inres ? w.batch_cnt : nullptr, w.batch_rq, cam, W, out, (uint32_t*)nullptr,
                      zcount, w.batch_state, w.inres);
   if (ev) (void)hipEventRecord(ev[1], stream);
   enqueue_phase_c(sc, cam, stage_fits(s), W, H, maxrec, out, w, zcount, stream);
