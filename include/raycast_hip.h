@@ -337,6 +337,12 @@ typedef struct rc_tuning {
   int headb_first;        /* one frame at a time: resolver workgroups that skip the whole-
                              workgroup queue of long regular segments and start at once on the
                              per-wave queue, whose front holds the runs that can be dense    */
+  int early_team;         /* one frame at a time: 1 = once a frame of the same scene, size and
+                             depth has shown where its long carry segments end, render those
+                             rows first and resolve their long segments (a team-only grid)
+                             while phase A of the rest of the image runs                     */
+  int band_rows;          /* test aid (with early_team): the early team's band, in rows, for
+                             every frame instead of the hint (0 = the hint)                   */
 } rc_tuning;
 void rc_default_tuning(rc_tuning *t);
 int rc_set_tuning(const rc_tuning *t);

@@ -83,6 +83,8 @@ rc_tuning default_tuning() {
   // so the dense runs reach the helpers ~0.5 ms earlier and the team segment alone bounds the
   // resolver (lone quadric 4096^2 4.66 -> 4.55-4.56 ms; profiles/r05e_lone_headb.txt)
   t.headb_first = 24;
+  t.early_team = 0;
+  t.band_rows = 0;
   return t;
 }
 rc_tuning g_tune = default_tuning();
@@ -109,7 +111,7 @@ const char* spin_site(int code) {
   return code >= 1 && code <= 4 ? site[code] : "?";
 }
 
-int FrameLog::enqueue(const void* team, hipStream_t st) {
+int FrameLog::enqueue(const void* team, hipStream_t st, long long k) {
   if (!ring) {
     HIP_TRY(hipHostMalloc((void**)&ring, kRing * sizeof(Entry), hipHostMallocDefault));
     for (int i = 0; i < kRing; ++i) ring[i].code = kPending;
@@ -120,6 +122,7 @@ int FrameLog::enqueue(const void* team, hipStream_t st) {
   }
   Entry* e = &ring[head % kRing];
   ((volatile Entry*)e)->code = kPending;
+  key[head % kRing] = k;
   HIP_TRY(hipMemcpyAsync(e, team, sizeof(Entry), hipMemcpyDeviceToHost, st));
   ++head;
   return 0;
@@ -147,6 +150,10 @@ long long FrameLog::poll() {
     if (e->clock_mhz > 0) {
       if (diag.clock_min == 0 || e->clock_mhz < diag.clock_min) diag.clock_min = e->clock_mhz;
       if (e->clock_mhz > diag.clock_max) diag.clock_max = e->clock_mhz;
+    }
+    if (code == 0) {   // a verified frame's long-segment extent: the next frame's band hint
+      hint_key = key[tail % kRing];
+      hint_row = e->team_row;
     }
     e->code = kPending;
     ++tail;
@@ -599,7 +606,7 @@ int rc_set_tuning(const rc_tuning* t) {
       in(t->block_min, 0, 1 << 30) && in(t->pipe_inres, 0, 2) && in(t->x0, 0, 1) &&
       in(t->resolve_clean, 1, 64) && in(t->shard_lone, 0, 1) && in(t->team_cscan, 0, 1) &&
       in(t->pipe_order, 0, 3) && in(t->pipe_helpers, 0, rc::kDenseSlots) &&
-      in(t->patch_host, 0, 2) && in(t->share_device, 0, 1) && in(t->headb_first, 0, 1 << 16) &&
+      in(t->patch_host, 0, 2) && in(t->share_device, 0, 1) && in(t->headb_first, 0, 1 << 16) && in(t->early_team, 0, 1) && in(t->band_rows, 0, 1 << 30) &&
       !(t->split_shade && !t->side);
   if (!ok) {
     std::fprintf(stderr, "Error: rc_set_tuning: a field is out of range\n");
@@ -953,8 +960,58 @@ int enqueue_render_ws(DevCtx& c, const rc_scene* s, int W, int H, int row0, int 
   if (maxrec < 3) w.inres = 0;
   w.patch = patch;
   w.inject = take_inject();
+  // The early team: the previous verified frame of this scene, size and depth had its long
+  // carry segments end by row `last`; this frame renders rows [0, last + 3) first and starts a
+  // team-only resolver on their list while phase A of the rest runs (launch_parity).  The band
+  // is only a schedule: the list is cut at the band's last writer, so the image is the same
+  // for any band (a long segment the band misses is resolved by the rest of the frame, and
+  // bit 30 of the frame's record then turns the hint off).
+  const rc_tuning tu = tune();
+  const long long key = ((long long)(uintptr_t)c.fb.scene_src * 1000003ll) ^
+                        ((long long)W << 40) ^ ((long long)H << 20) ^ (long long)maxrec;
+  int band = 0;
+  if (tu.early_team && w.inres && !w.side && w.team_blocks > 0 && !w.trace &&
+      c.lone_log.hint_key == key) {
+    const int hr = c.lone_log.hint_row;
+    const int last = (hr & 0x3fffffff) - 1;
+    if (!(hr & (1 << 30)) && last >= 0 && last + 3 < H * 3 / 4) band = last + 3;
+  }
+  // test aid: a forced band (any row count: the image does not depend on it)
+  if (tu.early_team && tu.band_rows > 0 && w.inres && !w.side && w.team_blocks > 0 && !w.trace)
+    band = tu.band_rows < H ? tu.band_rows : 0;
+  if (band > 0) {
+    const size_t P = (size_t)W * H;
+    if (c.fb.band.ensure(256) || c.fb.seg_start0.ensure(P * sizeof(int)) ||
+        c.fb.seg_key0.ensure(P * sizeof(long long)) ||
+        c.fb.seg_order0.ensure((size_t)rc::kSegOrderMax * sizeof(int))) {
+      std::fprintf(stderr, "Error: out of device memory for the parity workspace\n");
+      return -1;
+    }
+    if (!c.tstream) {
+      HIP_TRY(hipStreamCreateWithFlags(&c.tstream, hipStreamNonBlocking));
+      HIP_TRY(hipEventCreateWithFlags(&c.e0, hipEventDisableTiming));
+      HIP_TRY(hipEventCreateWithFlags(&c.et, hipEventDisableTiming));
+    }
+    w.band_rows = band;
+    w.team_grid = w.team_blocks;     // the early team: its own grid, one workgroup per CU
+    w.team_blocks = 0;               // the rest of the frame has no team of its own
+    w.resolve_blocks -= w.team_grid; // and runs on the CUs the early team leaves
+    if (w.helpers > w.resolve_blocks / 2) w.helpers = w.resolve_blocks / 2;
+    if (w.headb_first > w.resolve_blocks - w.helpers) w.headb_first = w.resolve_blocks - w.helpers;
+    w.counters0 = (int*)c.fb.band.p;
+    w.pcut = (long long*)((char*)c.fb.band.p + 128);
+    w.seg_start0 = (int*)c.fb.seg_start0.p;
+    w.seg_key0 = (long long*)c.fb.seg_key0.p;
+    w.seg_order0 = (int*)c.fb.seg_order0.p;
+    w.tstream = c.tstream;
+    w.e0 = c.e0;
+    w.et = c.et;
+    c.lone_band = band;
+  } else {
+    c.lone_band = 0;
+  }
   HIP_TRY(rc::launch_parity(ls, W, H, maxrec, d_out, w, zc, stream, timed ? ev + 1 : nullptr));
-  return c.lone_log.enqueue(w.team, stream);
+  return c.lone_log.enqueue(w.team, stream, key);
 }
 
 // After a synchronised parity render: the resolver's and phase C's bounded spins set

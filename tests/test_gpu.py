@@ -74,7 +74,9 @@ SCHEDULES = {"no-side": dict(side=0), "side-always": dict(side=1), "side-by-size
              "serial-plain-d2h": dict(overlap_d2h=0, staged_d2h=0, prefault=0),
              "device-patch": dict(patch_host=0),
              "mapped-patch-after-frame": dict(patch_host=1),
-             "helpers-8-hand-run-512": dict(helpers=8, hand_run=512)}
+             "helpers-8-hand-run-512": dict(helpers=8, hand_run=512),
+             "no-headb-first": dict(headb_first=0), "early-team": dict(early_team=1),
+             "early-band-300": dict(early_team=1, band_rows=300)}
 
 
 @pytest.mark.parametrize("sched", list(SCHEDULES))
@@ -740,3 +742,42 @@ def test_resolver_diagnostics_record(scenes, table):
     assert d["frames"] == 3 and 300 <= d["clock_mhz_min"] <= d["clock_mhz_max"] <= 3500, d
     assert d["wg_per_cu"] <= d["wg_per_cu_max"]
     assert p3_md5(out.cpu().numpy()) == want
+
+
+@pytest.mark.parametrize("key", ["quadric:4096x4096:d6:parity", "simple:1024x1024:d6:parity",
+                                 "reflection:2048x2048:d4:parity", "quadric:1024x1024:d6:parity",
+                                 "quadric:8192x8192:d6:parity", "quadric:333x517:d6:parity"])
+def test_early_team(key, scenes, table):
+    """Lone frames with the early team (rc_tuning.early_team): the first frame of a scene, size
+    and depth records where its long carry segments end; the next ones render those rows first
+    and resolve their long segments on a team-only grid while phase A of the rest runs (the
+    band's list cut at its last writer).  Every frame md5-equal to the reference, through the
+    drop-in path (rc_render) and device-resident (rc_render_device), and every hand-off
+    verified."""
+    torch = pytest.importorskip("torch")
+    scene, size, d, mode = key.split(":")
+    w, h = map(int, size.split("x"))
+    want = table[key]["md5"]
+    with rc.tuned(early_team=1):
+        for i in range(3):
+            assert p3_md5(rc.render(scenes[scene], w, h, depth=int(d[1:]), mode=mode)) == want, i
+        out = torch.empty((h, w, 3), dtype=torch.uint8, device="cuda")
+        for i in range(2):
+            rc.render_device(scenes[scene], w, h, out.data_ptr(), depth=int(d[1:]), mode=mode)
+            torch.cuda.synchronize()
+            assert p3_md5(out.cpu().numpy()) == want, ("device", i)
+    chk = rc.lone_frames_check()
+    assert chk["failed"] == 0
+
+
+@pytest.mark.parametrize("band", [1, 100, 161, 204, 369, 370, 512, 1023])
+def test_early_team_forced_bands(band, scenes, table):
+    """Forced early-team bands (rc_tuning.band_rows) anywhere in simple 1024^2 d6, whose 88k-entry
+    long segment runs over rows 161-369: a band that ends inside it (204: the cut that broke
+    round 3's two-band attempt) leaves the segment to the rest of the frame, which resolves it
+    with a whole workgroup; the image is the same for every band."""
+    key = "simple:1024x1024:d6:parity"
+    with rc.tuned(early_team=1, band_rows=band):
+        for i in range(2):
+            assert p3_md5(rc.render(scenes["simple"], 1024, 1024, depth=6)) == table[key]["md5"], i
+    assert rc.lone_frames_check()["failed"] == 0
