@@ -1078,7 +1078,11 @@ double event_ms(hipEvent_t a, hipEvent_t b) {
   return ms;
 }
 
-void fill_device_timing(DevCtx& c, const rc_options* opt, rc_timing* t) {
+// tail (optional): the frame's zero-normalize count (8 B) and counters[0..3] (at +16), copied
+// into pinned memory on the frame's stream behind its last kernel (rc_render), so reading them
+// costs no extra round trip after the frame
+void fill_device_timing(DevCtx& c, const rc_options* opt, rc_timing* t,
+                        const uint8_t* tail) {
   const bool parity = opt->mode == RC_MODE_PARITY && opt->max_recursion > 1;
   hipEvent_t* ev = c.ev[0];
   double k = parity ? event_ms(ev[0], ev[4]) : event_ms(ev[0], ev[1]);
@@ -1087,12 +1091,18 @@ void fill_device_timing(DevCtx& c, const rc_options* opt, rc_timing* t) {
   t->kernel_ms = k;
   t->resolve_ms = parity ? event_ms(ev[2], ev[3]) : 0.0;
   unsigned long long z = 0;
-  if (hipMemcpy(&z, c.fb.zcount.p, sizeof z, hipMemcpyDeviceToHost) == hipSuccess)
-    t->zero_normalize = (int64_t)z;
+  if (tail)
+    std::memcpy(&z, tail, sizeof z);
+  else if (hipMemcpy(&z, c.fb.zcount.p, sizeof z, hipMemcpyDeviceToHost) != hipSuccess)
+    z = 0;
+  t->zero_normalize = (int64_t)z;
   if (parity) {
     int cnt[4] = {0, 0, 0, 0};
-    if (hipMemcpy(cnt, c.fb.counters.p, sizeof cnt, hipMemcpyDeviceToHost) == hipSuccess)
-      t->dep_pixels = cnt[2];
+    if (tail)
+      std::memcpy(cnt, tail + 16, sizeof cnt);
+    else if (hipMemcpy(cnt, c.fb.counters.p, sizeof cnt, hipMemcpyDeviceToHost) != hipSuccess)
+      cnt[2] = 0;
+    t->dep_pixels = cnt[2];
 #if RC_DIAG
     if (std::getenv("RC_SIDE_STATS")) {
       int cc[16];
@@ -1760,6 +1770,12 @@ int rc_render(const rc_scene* s, int W, int H, const rc_options* opt, uint8_t* p
   } unset;
   if (E2eTrace::on()) g_e2e = &trace;
   if (enqueue_render(*c, s, W, H, 0, 1, H, opt, d_out, c->stream, true, patch, &ev)) return -1;
+  // the frame's counts for rc_timing / raycast()'s stderr lines, behind its last kernel
+  if (!c->pin_tail) HIP_TRY(hipHostMalloc((void**)&c->pin_tail, 64, hipHostMallocDefault));
+  HIP_TRY(hipMemcpyAsync(c->pin_tail, c->fb.zcount.p, 8, hipMemcpyDeviceToHost, c->stream));
+  if (parity)
+    HIP_TRY(hipMemcpyAsync(c->pin_tail + 16, c->fb.counters.p, 16, hipMemcpyDeviceToHost,
+                           c->stream));
   trace.mark(0);
   prefault(*c, pixmap, (size_t)H * row_bytes, tu);
   trace.mark(1);
@@ -1783,13 +1799,13 @@ int rc_render(const rc_scene* s, int W, int H, const rc_options* opt, uint8_t* p
   }
   c->lone_log.poll();
   if (timing) {
-    fill_device_timing(*c, opt, timing);
+    fill_device_timing(*c, opt, timing, c->pin_tail);
     timing->d2h_ms =
         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - td).count();
     timing->total_ms =
         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   } else {
-    fill_device_timing(*c, opt, nullptr);
+    fill_device_timing(*c, opt, nullptr, c->pin_tail);
   }
   trace.mark(7);
   trace.print();

@@ -196,6 +196,7 @@ struct DevCtx {
   uint8_t* pin_patch = nullptr;   // pinned: DEP entries' packed RGB
   size_t pin_bytes = 0;           // capacity of each pinned buffer, in entries
   int* pin_cnt = nullptr;         // pinned: counters[0..3]
+  uint8_t* pin_tail = nullptr;    // pinned: rc_render's frame counts (fill_device_timing)
   uint32_t* host_patch = nullptr;     // pinned, mapped: phase C's packed RGB per DEP entry
   uint32_t* host_patch_dev = nullptr; // its device address (patch_host)
   size_t host_patch_entries = 0;
@@ -242,7 +243,8 @@ int enqueue_render(DevCtx& c, const rc_scene* s, int W, int H, int row0, int row
                    const rc_options* opt, uint8_t* d_out, hipStream_t stream, bool timed,
                    uint32_t* patch = nullptr, hipEvent_t** evset = nullptr);
 int check_spin_error(FrameBufs& b, const rc_options* opt);
-void fill_device_timing(DevCtx& c, const rc_options* opt, rc_timing* t);
+void fill_device_timing(DevCtx& c, const rc_options* opt, rc_timing* t,
+                        const uint8_t* tail = nullptr);
 // rc_shard.hip: rc_render's multi-GPU path (a cached in-process group over devices
 // first..first+n-1, or n ranks sharing device `first` with device copies between them when
 // `share`); *d_image = the root's de-interleaved image.  The caller holds no lock.
