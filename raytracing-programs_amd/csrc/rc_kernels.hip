@@ -1742,9 +1742,10 @@ __device__ __forceinline__ bool batch_carries(CinG* cin, int ndep, int b, unsign
 }
 
 // Phase C of one batch of 64 DEP entries.  Under dep_fast phase A left each entry's primary
-// shade in wcarry[p] and counted the events of its primary part: a clean entry (no level hit
-// at its carry-in) is exactly that shade (every level's shade is zero, C/raycast.c:366-378),
-// the others resume at level 2 (shade_dep_cont).  Otherwise the pixel is recomputed.
+// shade in its DEP line (deprec[p].px..pz) and counted the events of its primary part: a
+// clean entry (no level hit at its carry-in) is exactly that shade (every level's shade is
+// zero, C/raycast.c:366-378), the others resume at level 2 (shade_dep_cont).  Otherwise the
+// pixel is recomputed.
 __device__ __forceinline__ void shade_batch(const Scene& sc, const Cam& cam, int W, int maxrec,
                                             const long long* __restrict__ dep_pix,
                                             const DepLine* __restrict__ deprec, int ndep, int b,
@@ -2931,8 +2932,8 @@ __global__ void __launch_bounds__(256) k_shard_rows(const RowShard* __restrict__
 }
 
 // Root, one wave per image row: the row's entries in scan order -> the resolver's inputs, in a
-// lone frame's layout (image pixel indices): the record at deprec[pixel], dep_pix = the
-// pixels in scan order, the entry's primary shade at wcarry[pixel] and every segment's key =
+// lone frame's layout (image pixel indices): the DEP line (record and primary shade) at
+// deprec[pixel], dep_pix = the pixels in scan order and every segment's key =
 // the image pixel of the writer before it, whose carry-out goes to wcarry[writer] (a DEP
 // pixel and a writer are never the same pixel).  The resolver, phase C inside it and its
 // framebuffer stores then run exactly as in a lone frame, into the root's image.  A segment
