@@ -438,12 +438,24 @@ __device__ __forceinline__ void stage_row_chunk(const uint8_t* __restrict__ src,
   }
 }
 
-// One workgroup of 1024: chunks of 4096 rows, four consecutive rows per thread (their loads
-// issued together), a thread-level pass, block scans of the thread totals + a chunk carry.
-// (One row per thread took four dependent load/scan/store rounds at 4096 rows: 16 us.)
-constexpr int kScanRows = 4;
+// The one-workgroup kernels of the compaction (k_row_scan, k_seg_order, k_band_cut) run as
+// kScanBlock threads.  With frames in flight they are dispatched beside the next frame's
+// phase A, whose workgroups (4 waves of 128 VGPRs) refill every CU slot they free: a
+// 1024-thread workgroup needs a whole CU's wave slots at once and waited 0.05-1.2 ms for one
+// (k_row_scan 0.164 ms mean in flight against 13 us alone, profiles/r05_rocprof_headline_...),
+// holding the frame's resolver back; 256 threads fit the slot one phase A workgroup frees.
+// k_row_scan: chunks of kScanBlock * kScanRows rows, kScanRows consecutive rows per thread
+// (their loads issued together), a thread-level pass, block scans of the thread totals + a
+// chunk carry.  (One row per thread took four dependent load/scan/store rounds at 4096 rows:
+// 16 us.)
+#ifndef RC_SCAN_BLOCK
+#define RC_SCAN_BLOCK 256
+#endif
+constexpr int kScanBlock = RC_SCAN_BLOCK;
+constexpr int kScanRows = kScanBlock >= 1024 ? 4 : 8;
+static_assert(kScanBlock % 64 == 0 && kScanBlock <= 1024, "whole waves, at most 16");
 
-// block-wide exclusive scan of (sum, max, max) over the 1024 threads; returns the block
+// block-wide exclusive scan of (sum, max, max) over the workgroup; returns the block
 // totals in t_cnt / t_w / t_d
 __device__ __forceinline__ void block_scan3(int& cnt, long long& lw, long long& ld, int* w_cnt,
                                             long long* w_w, long long* w_d, int& t_cnt,
@@ -570,7 +582,7 @@ __device__ __forceinline__ void row_scan_body(int H, const RowStats* __restrict_
   }
 }
 
-__global__ void __launch_bounds__(1024) k_row_scan(int H, const RowStats* __restrict__ rs,
+__global__ void __launch_bounds__(kScanBlock) k_row_scan(int H, const RowStats* __restrict__ rs,
                                                    int* __restrict__ row_off,
                                                    int* __restrict__ row_soff,
                                                    long long* __restrict__ row_prevw,
@@ -754,8 +766,8 @@ __global__ void __launch_bounds__(256) k_row_compact(
 // later one starts at p or after it, in band 1).  After k_row_stats over the band's rows: p,
 // the stats of p's row recomputed as if every pixel at or after p were class ident, the rows
 // after it emptied, and *pcut = p (0 when the band has no writer: an empty band-0 list).
-// One workgroup of 1024.
-__global__ void __launch_bounds__(1024) k_band_cut(const uint8_t* __restrict__ cls, int W,
+// One workgroup of kScanBlock.
+__global__ void __launch_bounds__(kScanBlock) k_band_cut(const uint8_t* __restrict__ cls, int W,
                                                    int R0, RowStats* __restrict__ rs,
                                                    long long* __restrict__ pcut) {
   __shared__ unsigned long long s_p;
@@ -1221,7 +1233,7 @@ __device__ __forceinline__ bool cin_get(CinG* cin, int j, unsigned tag, V3& c, b
 // The order's first counters[14] segments have >= block_min entries (rounded up to the
 // bucket width): k_resolve's workgroups take them from head A (counters[1]) while its waves
 // start on the rest from head B (counters[15]).
-__global__ void __launch_bounds__(1024) k_seg_order(const int* __restrict__ seg_start,
+__global__ void __launch_bounds__(kScanBlock) k_seg_order(const int* __restrict__ seg_start,
                                                      int* __restrict__ counters,
                                                      int* __restrict__ order,
                                                      int* __restrict__ batch_state,
@@ -3107,15 +3119,15 @@ hipError_t launch_parity(const LaunchScene& s, int W, int H, int maxrec, uint8_t
     hipLaunchKernelGGL(k_row_stats, dim3(rb0), dim3(256), 0, stream, w.cls, W, R0,
                        (RowStats*)w.row_stats, w.counters0, (uint4*)w.team,
                        (int)(sizeof(TeamState) / sizeof(uint4)), w.batch_state, w.batch_ints);
-    hipLaunchKernelGGL(k_band_cut, dim3(1), dim3(1024), 0, stream, w.cls, W, R0,
+    hipLaunchKernelGGL(k_band_cut, dim3(1), dim3(kScanBlock), 0, stream, w.cls, W, R0,
                        (RowStats*)w.row_stats, w.pcut);
-    hipLaunchKernelGGL(k_row_scan, dim3(1), dim3(1024), 0, stream, R0,
+    hipLaunchKernelGGL(k_row_scan, dim3(1), dim3(kScanBlock), 0, stream, R0,
                        (const RowStats*)w.row_stats, w.row_off, w.row_soff, w.row_prevw,
                        w.row_prevd, w.counters0);
     hipLaunchKernelGGL(k_row_compact, dim3(rb0), dim3(256), 0, stream, w.cls, W, R0, w.row_off,
                        w.row_soff, w.row_prevw, w.row_prevd, w.dep_pix, w.seg_start0, w.seg_key0,
                        (const long long*)w.pcut);
-    hipLaunchKernelGGL(k_seg_order, dim3(1), dim3(1024), 0, stream, w.seg_start0, w.counters0,
+    hipLaunchKernelGGL(k_seg_order, dim3(1), dim3(kScanBlock), 0, stream, w.seg_start0, w.counters0,
                        w.seg_order0, w.batch_state, w.batch_cnt, w.batch_rq, 0, 0, 0);
     (void)hipEventRecord(w.e0, stream);
     (void)hipStreamWaitEvent(w.tstream, w.e0, 0);
@@ -3139,13 +3151,13 @@ hipError_t launch_parity(const LaunchScene& s, int W, int H, int maxrec, uint8_t
     const int row_blocks = (H + kRowWaves - 1) / kRowWaves;
     hipLaunchKernelGGL(k_row_stats, dim3(row_blocks), dim3(256), 0, stream, w.cls, W, H,
                        (RowStats*)w.row_stats, w.counters, (uint4*)nullptr, 0, (int*)nullptr, 0);
-    hipLaunchKernelGGL(k_row_scan, dim3(1), dim3(1024), 0, stream, H,
+    hipLaunchKernelGGL(k_row_scan, dim3(1), dim3(kScanBlock), 0, stream, H,
                        (const RowStats*)w.row_stats, w.row_off, w.row_soff, w.row_prevw,
                        w.row_prevd, w.counters);
     hipLaunchKernelGGL(k_row_compact, dim3(row_blocks), dim3(256), 0, stream, w.cls, W, H,
                        w.row_off, w.row_soff, w.row_prevw, w.row_prevd, w.dep_pix, w.seg_start,
                        w.seg_key, (const long long*)nullptr);
-    hipLaunchKernelGGL(k_seg_order, dim3(1), dim3(1024), 0, stream, w.seg_start, w.counters,
+    hipLaunchKernelGGL(k_seg_order, dim3(1), dim3(kScanBlock), 0, stream, w.seg_start, w.counters,
                        w.seg_order, w.batch_state, w.batch_cnt, w.batch_rq, w.block_min,
                        w.resolve_blocks - w.team_blocks - w.helpers - w.headb_first, 0);
     if (ev) (void)hipEventRecord(ev[1], stream);
@@ -3186,12 +3198,12 @@ hipError_t launch_parity(const LaunchScene& s, int W, int H, int maxrec, uint8_t
   hipLaunchKernelGGL(k_row_stats, dim3(row_blocks), dim3(256), 0, stream, w.cls, W, H,
                      (RowStats*)w.row_stats, w.counters, (uint4*)w.team,
                      (int)(sizeof(TeamState) / sizeof(uint4)), w.batch_state, w.batch_ints);
-  hipLaunchKernelGGL(k_row_scan, dim3(1), dim3(1024), 0, stream, H, (const RowStats*)w.row_stats,
+  hipLaunchKernelGGL(k_row_scan, dim3(1), dim3(kScanBlock), 0, stream, H, (const RowStats*)w.row_stats,
                      w.row_off, w.row_soff, w.row_prevw, w.row_prevd, w.counters);
   hipLaunchKernelGGL(k_row_compact, dim3(row_blocks), dim3(256), 0, stream, w.cls, W, H,
                      w.row_off, w.row_soff, w.row_prevw, w.row_prevd, w.dep_pix, w.seg_start,
                      w.seg_key);
-  hipLaunchKernelGGL(k_seg_order, dim3(1), dim3(1024), 0, stream, w.seg_start, w.counters,
+  hipLaunchKernelGGL(k_seg_order, dim3(1), dim3(kScanBlock), 0, stream, w.seg_start, w.counters,
                      w.seg_order, w.batch_state, w.batch_cnt, w.batch_rq, w.block_min,
                      block_cap, w.batch_ints > 0 ? 0 : 1);
   // resolve_lds > 80 KiB keeps one resolver block (4 waves, one per SIMD) per CU: the chain
@@ -3362,7 +3374,7 @@ hipError_t launch_shard_local(const LaunchScene& s, int W, int H, int row0, int 
   const int row_blocks = (nrows + kRowWaves - 1) / kRowWaves;
   hipLaunchKernelGGL(k_row_stats, dim3(row_blocks), dim3(256), 0, stream, w.cls, W, nrows,
                      (RowStats*)w.row_stats, nullptr, nullptr, 0, nullptr, 0);
-  hipLaunchKernelGGL(k_row_scan, dim3(1), dim3(1024), 0, stream, nrows,
+  hipLaunchKernelGGL(k_row_scan, dim3(1), dim3(kScanBlock), 0, stream, nrows,
                      (const RowStats*)w.row_stats, w.row_off, w.row_soff, w.row_prevw,
                      w.row_prevd, w.counters);
   hipLaunchKernelGGL(k_shard_pack, dim3(row_blocks), dim3(256), 0, stream, w.cls,
@@ -3386,7 +3398,7 @@ hipError_t launch_shard_resolve(const LaunchScene& s, int W, int H, int G, int r
   (void)hipMemsetAsync(w.team, 0, sizeof(TeamState), stream);
   hipLaunchKernelGGL(k_shard_rows, dim3((H + 255) / 256), dim3(256), 0, stream, rs, G, rmax, H,
                      (RowStats*)w.row_stats);
-  hipLaunchKernelGGL(k_row_scan, dim3(1), dim3(1024), 0, stream, H, (const RowStats*)w.row_stats,
+  hipLaunchKernelGGL(k_row_scan, dim3(1), dim3(kScanBlock), 0, stream, H, (const RowStats*)w.row_stats,
                      w.row_off, w.row_soff, w.row_prevw, w.row_prevd, w.counters);
   const int row_blocks = (H + kRowWaves - 1) / kRowWaves;
   hipLaunchKernelGGL(k_shard_unpack, dim3(row_blocks), dim3(256), 0, stream, rs,
@@ -3394,7 +3406,7 @@ hipError_t launch_shard_resolve(const LaunchScene& s, int W, int H, int G, int r
                      w.row_off, w.row_soff,
                      w.row_prevw, w.row_prevd, (DepLine*)w.deprec, w.dep_pix, w.seg_start,
                      w.seg_key, w.wcarry, bound, thin0);
-  hipLaunchKernelGGL(k_seg_order, dim3(1), dim3(1024), 0, stream, w.seg_start, w.counters,
+  hipLaunchKernelGGL(k_seg_order, dim3(1), dim3(kScanBlock), 0, stream, w.seg_start, w.counters,
                      w.seg_order, w.batch_state, w.batch_cnt, w.batch_rq, w.block_min,
                      w.resolve_blocks - w.team_blocks - w.helpers - w.headb_first, 1);
   if (ev) (void)hipEventRecord(ev[0], stream);
