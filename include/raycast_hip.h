@@ -343,6 +343,8 @@ typedef struct rc_tuning {
                              while phase A of the rest of the image runs                     */
   int band_rows;          /* test aid (with early_team): the early team's band, in rows, for
                              every frame instead of the hint (0 = the hint)                   */
+  int pipe_last_whole;    /* rc_frames_wait runs the window's last frame's phase C on every CU
+                             instead of the pixel partition (1, default; 0 = the partition)   */
 } rc_tuning;
 void rc_default_tuning(rc_tuning *t);
 int rc_set_tuning(const rc_tuning *t);

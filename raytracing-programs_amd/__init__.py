@@ -119,7 +119,7 @@ TUNING_FIELDS = ["side", "split_shade", "resolve_shared", "resolve_lds_kb", "res
                  "block_min", "pipe_inres", "x0", "resolve_clean",
                  "shard_lone", "team_cscan", "pipe_order", "pipe_helpers", "patch_host",
                  "share_device", "headb_first", "early_team",
-                 "band_rows"]
+                 "band_rows", "pipe_last_whole"]
 
 
 class RcTuning(ctypes.Structure):

@@ -85,6 +85,7 @@ rc_tuning default_tuning() {
   t.headb_first = 24;
   t.early_team = 0;
   t.band_rows = 0;
+  t.pipe_last_whole = 1;
   return t;
 }
 rc_tuning g_tune = default_tuning();
@@ -606,7 +607,7 @@ int rc_set_tuning(const rc_tuning* t) {
       in(t->block_min, 0, 1 << 30) && in(t->pipe_inres, 0, 2) && in(t->x0, 0, 1) &&
       in(t->resolve_clean, 1, 64) && in(t->shard_lone, 0, 1) && in(t->team_cscan, 0, 1) &&
       in(t->pipe_order, 0, 3) && in(t->pipe_helpers, 0, rc::kDenseSlots) &&
-      in(t->patch_host, 0, 2) && in(t->share_device, 0, 1) && in(t->headb_first, 0, 1 << 16) && in(t->early_team, 0, 1) && in(t->band_rows, 0, 1 << 30) &&
+      in(t->patch_host, 0, 2) && in(t->share_device, 0, 1) && in(t->headb_first, 0, 1 << 16) && in(t->early_team, 0, 1) && in(t->band_rows, 0, 1 << 30) && in(t->pipe_last_whole, 0, 1) &&
       !(t->split_shade && !t->side);
   if (!ok) {
     std::fprintf(stderr, "Error: rc_set_tuning: a field is out of range\n");
@@ -1319,6 +1320,29 @@ void pipe_release_all() {
   for (auto& c : g_ctx) pipe_release(c);
 }
 
+// The pending phase C (Pipe::cdefer) of the last submitted frame: on its lane's phase C
+// stream, or with `whole` on the device stream over every CU — the window's last frame, whose
+// phase C otherwise ran alone on the pixel partition after the last resolver (0.8 ms of a
+// 20-frame window's drain at quadric 4096^2 against ~0.47 ms on every CU).
+int flush_phase_c(DevCtx& c, bool whole) {
+  Pipe& p = c.pipe;
+  if (!p.cdefer) return 0;
+  p.cdefer = false;
+  rc::ParityWork& w = p.cdefer_w;
+  hipStream_t s = p.pc[p.cdefer_lane];
+  if (whole) {
+    s = c.stream;
+    w.phase_c_blocks = c.cus * 8;
+  }
+  HIP_TRY(rc::launch_phase_c(p.cdefer_ls, p.cdefer_W, p.cdefer_H, p.cdefer_maxrec, p.cdefer_out,
+                             w, p.cdefer_zc, s));
+  // the frame's hand-off words, before the event that lets slot k's next frame reset them
+  if (p.log.enqueue(w.team, s)) return -1;
+  HIP_TRY(hipEventRecord(p.cdone[p.cdefer_k], s));
+  p.cpend[p.cdefer_k] = true;
+  return 0;
+}
+
 int pipe_init(DevCtx& c, long long pixels) {
   Pipe& p = c.pipe;
   if (p.init) return 0;
@@ -1454,6 +1478,9 @@ int rc_frame_submit(const rc_scene* s, int W, int H, const rc_options* opt, uint
                  "rc_frames_wait\n", p.log.failed);
     return -1;
   }
+  // the previous frame's phase C on its lane (it was held back in case that frame was the
+  // window's last), before anything of this frame: the frame log stays in submission order
+  if (flush_phase_c(*c, false)) return -1;
   const int k = (int)(p.total % p.slots);
   const int lane = (int)(p.total % p.lanes);
   FrameBufs& b = p.fb[k];
@@ -1491,12 +1518,17 @@ int rc_frame_submit(const rc_scene* s, int W, int H, const rc_options* opt, uint
   w.rt1 = p.rt_on ? p.rt[e][1] : nullptr;
   w.inject = take_inject();
   HIP_TRY(rc::launch_parity(ls, W, H, maxrec, d_out, w, zc, st, nullptr));
-  if (p.fifo) {   // phase C on the lane's stream, after the resolver
-    HIP_TRY(rc::launch_phase_c(ls, W, H, maxrec, d_out, w, zc, p.pc[lane]));
-    // the frame's hand-off words, before the event that lets slot k's next frame reset them
-    if (p.log.enqueue(w.team, p.pc[lane])) return -1;
-    HIP_TRY(hipEventRecord(p.cdone[k], p.pc[lane]));
-    p.cpend[k] = true;
+  if (p.fifo) {   // phase C after the resolver: at the next submit or rc_frames_wait
+    p.cdefer = true;
+    p.cdefer_lane = lane;
+    p.cdefer_k = k;
+    p.cdefer_W = W;
+    p.cdefer_H = H;
+    p.cdefer_maxrec = maxrec;
+    p.cdefer_ls = ls;
+    p.cdefer_w = w;
+    p.cdefer_out = d_out;
+    p.cdefer_zc = zc;
   } else if (p.log.enqueue(w.team, st)) {   // slot streams: the frame ends on its slot's stream
     return -1;
   }
@@ -1516,8 +1548,9 @@ int rc_frames_wait(rc_timing* timing) {
   std::lock_guard<std::mutex> lk(c->mu);
   Pipe& p = c->pipe;
   if (timing) std::memset(timing, 0, sizeof *timing);
+  const int fl = p.init ? flush_phase_c(*c, tune().pipe_last_whole != 0) : 0;
   HIP_TRY(hipStreamSynchronize(c->stream));
-  int rc = 0;
+  int rc = fl;
   if (p.init) {
     for (int k = 0; k < p.slots; ++k)
       if (p.pix[k]) HIP_TRY(hipStreamSynchronize(p.pix[k]));

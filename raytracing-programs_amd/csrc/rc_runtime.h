@@ -156,6 +156,14 @@ struct Pipe {
   bool rt_on = true;                 // resolver timing events recorded (RC_PIPE_NO_RT: off)
   int built_lanes = 0, built_slots = 0, built_res = 0, built_order = 0;   // the tuning it was built with
   FrameLog log;                      // every pipelined parity frame, in submission order
+  // the last submitted parity frame's phase C: launched at the next submit (on its lane's
+  // phase C stream) or by rc_frames_wait (on every CU: nothing else is left to run beside it)
+  bool cdefer = false;
+  int cdefer_lane = 0, cdefer_k = 0, cdefer_W = 0, cdefer_H = 0, cdefer_maxrec = 0;
+  rc::LaunchScene cdefer_ls{};
+  rc::ParityWork cdefer_w{};
+  uint8_t* cdefer_out = nullptr;
+  unsigned long long* cdefer_zc = nullptr;
 };
 
 struct DevCtx {

@@ -221,7 +221,8 @@ def test_tuning_api_validates():
                 dict(team_blocks=-2), dict(resolve_grid=4), dict(split_shade=1, side=0),
                 dict(copy_threads=0), dict(resolve_lds_kb=200), dict(long_len=10), dict(x0=2),
                 dict(pipe_order=4), dict(patch_host=3), dict(share_device=2),
-                dict(headb_first=-1), dict(early_team=2), dict(band_rows=-1)):
+                dict(headb_first=-1), dict(early_team=2), dict(band_rows=-1),
+                dict(pipe_last_whole=2)):
         with pytest.raises(ValueError):
             rc.set_tuning(**bad)
         assert rc.get_tuning() == base, bad
@@ -231,7 +232,7 @@ def test_tuning_api_validates():
     assert rc.get_tuning() == base
     # the round-5 fields round-trip, and their defaults are the measured schedule
     assert (base["share_device"], base["headb_first"], base["early_team"],
-            base["band_rows"]) == (0, 24, 0, 0)
+            base["band_rows"], base["pipe_last_whole"]) == (0, 24, 0, 0, 1)
     with rc.tuned(headb_first=0, early_team=1, band_rows=204, share_device=1):
         t = rc.get_tuning()
         assert (t["headb_first"], t["early_team"], t["band_rows"], t["share_device"]) == \

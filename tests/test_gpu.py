@@ -297,7 +297,8 @@ PIPES = {"default": {},
          "no-lane-helpers": dict(pipe_helpers=0),
          "lane-helpers-every-run": dict(pipe_helpers=8, hand_run=2),
          "stream-order-1": dict(pipe_order=1),
-         "queue-per-lane": dict(pipe_order=3)}
+         "queue-per-lane": dict(pipe_order=3),
+         "last-phase-c-on-partition": dict(pipe_last_whole=0)}
 
 
 @pytest.mark.parametrize("pipe", list(PIPES))
