@@ -339,6 +339,37 @@ def test_frames_in_flight(pipe, scenes, table):
     rc.pipe_reset()   # later tests get the default pipeline
 
 
+def test_random_scene_sweep_vs_oracle(tmp_path):
+    """Sixteen random phantom-safe scenes (2-12 shapes, one or two lights, odd sizes, depths
+    2-7) against the CPU oracle: one frame at a time (rc_render) and as one window of frames
+    in flight (rc_frame_submit, every scene's frame in one window, the last one's phase C on
+    every CU in rc_frames_wait).  Parity mode, where the scan-order carry chains are."""
+    torch = pytest.importorskip("torch")
+    rng = np.random.default_rng(2025)
+    cases = []
+    for seed in range(16):
+        path = str(tmp_path / f"r{seed}.scene")
+        random_scene(rng, path, int(rng.integers(2, 13)), int(rng.integers(1, 3)))
+        s = rc.Scene.from_file(path)
+        w, h, d = int(rng.integers(96, 320)), int(rng.integers(64, 256)), int(rng.integers(2, 8))
+        want, st = oracle_render(s, w, h, d, "parity")
+        if not st["parity_defined"]:
+            continue
+        np.testing.assert_array_equal(rc.render(s, w, h, depth=d, mode="parity"), want,
+                                      err_msg=f"scene {seed} {w}x{h} d{d}")
+        cases.append((seed, s, w, h, d, want,
+                      torch.zeros((h, w, 3), dtype=torch.uint8, device="cuda")))
+    assert len(cases) >= 8
+    torch.cuda.synchronize()
+    for seed, s, w, h, d, want, buf in cases:
+        rc.frame_submit(s, w, h, buf.data_ptr(), depth=d, mode="parity")
+    tim = {}
+    rc.frames_wait(tim)
+    assert (tim["frames_checked"], tim["frames_failed"]) == (len(cases), 0), tim
+    for seed, s, w, h, d, want, buf in cases:
+        np.testing.assert_array_equal(buf.cpu().numpy(), want, err_msg=f"in flight: scene {seed}")
+
+
 LIGHT = ("light, color: [1.5, 1.2, 1.0], radial-a2: 0.01, radial-a1: 0.0125, radial-a0: 0.0125, "
          "position: [3, 6, 1]\n")
 DEGENERATE = {
