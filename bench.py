@@ -79,7 +79,7 @@ def load_pkg():
 
 # rocprofv3 --pmc summaries of this exact configuration from HEAD (scripts/pmc_valu.sh,
 # scripts/pmc_fast.sh -> scripts/pmc_summary.py): per-kernel counter means per launch.
-PMC_PROFILES = {("quadric", 4096, 6, "parity"): "profiles/r05l_pmc_lone_4096.json",
+PMC_PROFILES = {("quadric", 4096, 6, "parity"): "profiles/r05fl_pmc_lone_4096.json",
                 ("reflection", 2048, 4, "parity"): "profiles/r03e_pmc_lone_c3.json",
                 ("quadric", 8192, 6, "parity"): "profiles/r03e_pmc_lone_c5.json",
                 ("quadric", 4096, 6, "fast"): "profiles/r02c_pmc_fast_4096.json"}
@@ -93,7 +93,7 @@ PMC_TRAFFIC_INFLIGHT = {("quadric", 4096, 6, "parity"): "profiles/r03f_pmc_traff
 # The headline's whole counter set from ONE command at HEAD (scripts/pmc_headline.sh: kernel
 # stats, VALU/wave-state and FETCH/WRITE passes of `bench.py --timed-only --steps 20 --warmup
 # 3`, the default frames in flight): valu_busy and traffic of the headline line come from it.
-PMC_HEADLINE = {("quadric", 4096, 6, "parity"): "profiles/r05_pmc_headline.json"}
+PMC_HEADLINE = {("quadric", 4096, 6, "parity"): "profiles/r05f_pmc_headline.json"}
 
 
 def pmc_kernel(kernel, scene, size, depth, mode, inflight=False):
