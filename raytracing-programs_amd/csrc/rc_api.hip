@@ -1561,12 +1561,15 @@ int rc_frames_wait(rc_timing* timing) {
     // every frame since the last wait, from its latched hand-off words (FrameLog)
     if (p.log.drain() > 0) rc = -1;
     long long checked = 0, failed = 0;
-    p.log.take(&checked, &failed);
+    p.log.take(&checked, &failed);   // the window's frames, also those an earlier poll read
+    if (failed > 0) rc = -1;
     if (timing) {
       timing->frames_checked = checked;
       timing->frames_failed = failed;
     }
-    for (int k = 0; k < p.slots; ++k) {   // the last frame of each slot, with the details
+    // the details of a failure from the last frame of each slot (the log already holds every
+    // frame's words: without a failure in the window there is nothing to read back)
+    for (int k = 0; failed > 0 && k < p.slots; ++k) {
       if (!p.used[k] || !p.fb[k].team.p) continue;
       if (report_spin_error(p.fb[k], "frames in flight")) rc = -1;
     }
