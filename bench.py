@@ -187,7 +187,8 @@ def run_leg_with_watchdog(leg, timeout_s, on_timeout):
     """Run leg() under a watchdog: if it has not returned after timeout_s (a stuck
     multi-process exchange), on_timeout() runs (rank 0 prints the line with the leg marked as
     timed out, so the timed result is not lost) and the process exits with LEG_TIMEOUT_EXIT —
-    never 0, so the driver sees the hang."""
+    never 0, so the driver sees the hang.  A leg that raises returns {"error": ...} instead
+    (the caller prints the line with it, then exits with LEG_TIMEOUT_EXIT as well)."""
     done = threading.Event()
 
     def watch():
@@ -202,6 +203,8 @@ def run_leg_with_watchdog(leg, timeout_s, on_timeout):
     threading.Thread(target=watch, daemon=True).start()
     try:
         return leg()
+    except Exception as e:  # noqa: BLE001 — reported in the line; the timed value stands
+        return {"error": f"{type(e).__name__}: {e}"}
     finally:
         done.set()
 
@@ -778,6 +781,11 @@ def main():
         if shard_leg_res:
             line["sharded_single_image"] = shard_leg_res
         print(json.dumps(line), flush=True)
+    if isinstance(shard_leg_res, dict) and "error" in shard_leg_res:
+        # the exchange failed on this rank: the others may be left inside a collective, so no
+        # teardown (it could block); the line is out, the status says the leg failed
+        sys.stdout.flush()
+        os._exit(LEG_TIMEOUT_EXIT)
     if group is not None:
         group.close()
     if multi:

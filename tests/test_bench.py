@@ -27,6 +27,20 @@ def test_watchdog_exits_nonzero_on_a_stuck_leg():
     assert "not reached" not in r.stdout
 
 
+def test_watchdog_reports_a_failing_leg():
+    """A leg that raises (an RCCL error in the sharded exchange) comes back as an error
+    record, so rank 0 can still print the line; the watchdog does not fire afterwards."""
+    calls = []
+
+    def leg():
+        raise RuntimeError("rc_render_sharded failed")
+    r = bench.run_leg_with_watchdog(leg, 0.2, lambda: calls.append(1))
+    assert r == {"error": "RuntimeError: rc_render_sharded failed"}
+    import time
+    time.sleep(0.4)
+    assert not calls
+
+
 def test_watchdog_returns_the_leg_result():
     calls = []
     assert bench.run_leg_with_watchdog(lambda: 42, 30, lambda: calls.append(1)) == 42
