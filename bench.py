@@ -422,17 +422,25 @@ def main():
     W = H = args.size
     mode = args.mode
     parity = mode == "parity" and args.depth > 0
-    group, group_err = None, None
-    if multi and backend == "nccl":
+    def join_group():
+        g, err = None, None
         try:
-            group = make_group(pkg, dist, world, rank, local)
+            g = make_group(pkg, dist, world, rank, local)
         except Exception as e:  # noqa: BLE001 — reported in the line; replicas still run
-            group_err = f"{type(e).__name__}: {e}"
-        ok = torch.tensor([0 if group is None else 1], dtype=torch.int32, device="cuda")
+            err = f"{type(e).__name__}: {e}"
+        ok = torch.tensor([0 if g is None else 1], dtype=torch.int32, device="cuda")
         dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-        if int(ok.item()) == 0 and group is not None:   # every rank or none uses the group
-            group.close()
-            group, group_err = None, group_err or "another rank failed to join the rc_group"
+        if int(ok.item()) == 0 and g is not None:   # every rank or none uses the group
+            g.close()
+            g, err = None, err or "another rank failed to join the rc_group"
+        return g, err
+
+    # the library's RCCL group before the timed steps only when the step needs it (fast mode's
+    # row shards, --shard); parity replicas join it after them, inside the watchdog-bounded
+    # sharded leg, so a communicator that never forms cannot cost the headline
+    group, group_err = None, None
+    if multi and backend == "nccl" and (mode in ("fast", "cuda") or args.shard):
+        group, group_err = join_group()
     # the step: fast mode over N GPUs = one image row-sharded (strong); parity over N GPUs =
     # N replicas, one image per GPU (weak: the carry resolver is serial), or the
     # sharded single image with --shard
@@ -733,6 +741,11 @@ def main():
     LEG_TIMEOUT_S = 120
 
     def shard_leg():
+        nonlocal group, group_err
+        if group is None:
+            group, group_err = join_group()
+            if group is None:
+                return {"error": f"no rc_group: {group_err}"}
         dist.barrier()
         group.render(scene, W, H, out.data_ptr(), depth=args.depth, mode=mode)   # warm
         dist.barrier()
@@ -775,7 +788,8 @@ def main():
             print(json.dumps(line), flush=True)
 
     shard_leg_res = None
-    if group is not None and not sharded and not args.timed_only:
+    if (multi and backend == "nccl" and not sharded and not args.timed_only
+            and group_err is None):
         shard_leg_res = run_leg_with_watchdog(shard_leg, LEG_TIMEOUT_S, leg_timed_out)
     if rank == 0:
         if shard_leg_res:
