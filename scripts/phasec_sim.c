@@ -7,7 +7,8 @@
  * nearest-hit costs n tests if any lane is still looping, a light's shadow loop costs the
  * most tests any lane at that level needs.  The entries are taken in k_dep_chunks' order
  * (1 024-entry chunks, hit entries compacted in order, 64 per wave) and, for comparison,
- * sorted by their per-level pattern within each chunk.
+ * sorted by their per-level pattern within each chunk.  It also prints the split of a hit
+ * entry's tests between the nearest-hit searches and the shadow rays.
  *
  *   gcc -O2 -ffp-contract=off -Iinclude -Ioracle -Iraytracing-programs_amd/csrc \
  *       scripts/phasec_sim.c raytracing-programs_amd/csrc/rc_scene.c -lm -o /tmp/phasec_sim
@@ -195,6 +196,16 @@ int main(int argc, char **argv) {
       c_sorted += wave_cost(lst + w0, nw, c.n, c.m);
     }
   }
+  long long nn = 0, ns = 0, nl = 0;
+  for (long long q = 0; q < ndep; ++q) {
+    if (!hitm[q]) continue;
+    nn += (long long)all[q].levels * c.n;
+    for (int l = 0; l < all[q].levels; ++l)
+      for (int li = 0; li < c.m && li < 4; ++li)
+        if (all[q].sh[l][li] > 0) ns += all[q].sh[l][li], ++nl;
+  }
+  printf("per hit entry: nearest-hit tests %.2f, shadow tests %.2f (%.2f lit lights)\n",
+         (double)nn / nhit, (double)ns / nhit, (double)nl / nhit);
   printf("DEP entries %lld, hit entries %lld, waves %lld\n", ndep, nhit, waves);
   printf("lockstep cost (shape tests per wave, mean): chunk order %.1f, sorted within chunks %.1f "
          "(%.1f %%), per-lane mean %.1f\n",
