@@ -364,9 +364,82 @@ def resolver_diag(d):
             "clock_mhz": {"min": d["clock_mhz_min"], "max": d["clock_mhz_max"]}}
 
 
+def free_port():
+    """A TCP port free on 127.0.0.1 right now (the rendezvous of self-launched ranks)."""
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_plan(n, argv, env, port):
+    """One (argv, env) per rank for `bench.py --gpus n` started without a launcher: the same
+    script and arguments in a fresh interpreter, with the variables torchrun would set
+    (RANK = LOCAL_RANK = r, WORLD_SIZE = n, rendezvous on 127.0.0.1:port).  The children are
+    started before this process makes any HIP call, and never by an exec of it."""
+    plans = []
+    for r in range(n):
+        e = dict(env)
+        e.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                 GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        plans.append(([sys.executable, "-u", os.path.abspath(__file__)] + list(argv), e))
+    return plans
+
+
+def worst_status(codes):
+    """The job's exit status from its ranks': 0 when every rank exited 0, else the largest
+    failure, a rank killed by signal s counting as 128 + s (the shell's convention)."""
+    norm = [(128 - c if c < 0 else c) for c in codes]
+    return max(norm) if norm else 0
+
+
+def run_ranks(plans, grace_s=60.0, poll_s=0.2):
+    """Start every rank, wait for all of them and return their exit codes.  Rank 0's JSON line
+    reaches the caller through the inherited stdout.  Once a rank has failed, the others get
+    grace_s to finish (they may be blocked in a collective with the dead rank) and are then
+    killed by their own PIDs."""
+    procs = [subprocess.Popen(a, env=e) for a, e in plans]
+    deadline = None
+    try:
+        while any(p.poll() is None for p in procs):
+            if deadline is None and any(p.returncode not in (None, 0) for p in procs):
+                deadline = time.monotonic() + grace_s
+            if deadline is not None and time.monotonic() > deadline:
+                for p in procs:
+                    if p.poll() is None:
+                        print(f"bench.py: rank pid {p.pid} still running {grace_s:.0f} s after "
+                              "another rank failed; killing it", file=sys.stderr, flush=True)
+                        p.kill()
+            time.sleep(poll_s)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+            p.wait()
+    return [p.returncode for p in procs]
+
+
+def resolve_world(gpus, env):
+    """(world size, launch children?) for `--gpus` (None = not given) under this environment.
+    Under a launcher (WORLD_SIZE set) --gpus must equal WORLD_SIZE; without one, --gpus N > 1
+    means this process launches the N ranks itself.  Raises ValueError on a mismatch."""
+    ws = env.get("WORLD_SIZE")
+    if ws is not None:
+        ws = int(ws)
+        if gpus is not None and gpus != ws:
+            raise ValueError(f"--gpus {gpus} but the launcher started WORLD_SIZE={ws} ranks")
+        return ws, False
+    n = 1 if gpus is None else gpus
+    if n < 1:
+        raise ValueError(f"--gpus {n}: need at least one GPU")
+    return n, n > 1
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (one rank each); default 1, or WORLD_SIZE under a launcher.  "
+                         "Without a launcher, N > 1 starts the N ranks as child processes")
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--mode", default="parity", choices=["parity", "fast", "cuda"],
@@ -394,16 +467,35 @@ def main():
                          "the step instead of N replicas")
     args = ap.parse_args()
 
+    try:
+        world, spawn = resolve_world(args.gpus, os.environ)
+    except ValueError as e:
+        print(f"bench.py: {e}", file=sys.stderr, flush=True)
+        sys.exit(2)
+    if spawn:   # no launcher: this process only starts the ranks (no torch, no HIP call here)
+        codes = run_ranks(launch_plan(world, sys.argv[1:], os.environ, free_port()))
+        if any(codes):
+            print(f"bench.py: rank exit codes {codes}", file=sys.stderr, flush=True)
+        sys.exit(worst_status(codes))
+
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     backend = os.environ.get("RC_BENCH_BACKEND", "nccl")   # gloo: 1-GPU rehearsal only
+    ndev = torch.cuda.device_count()
     if backend != "nccl":   # rehearsal: ranks share the GPUs, so no RCCL group (replicas only)
-        local %= max(1, torch.cuda.device_count())
+        local %= max(1, ndev)
+    elif local >= ndev:
+        print(f"bench.py: rank {rank} needs GPU {local} but {ndev} are visible (one rank per "
+              "GPU; RC_BENCH_BACKEND=gloo shares them for a rehearsal)", file=sys.stderr,
+              flush=True)
+        sys.exit(2)
     torch.cuda.set_device(local)
+    # host-side collectives (timing max, verification counts): on the device over RCCL, on the
+    # host over gloo
+    cdev = "cuda" if backend == "nccl" else "cpu"
     multi = world > 1 or args.force_group
     if multi:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -539,7 +631,7 @@ def main():
     if single:
         phases = single_phases
         single["resolve_ms_in_flight"] = round(pipe_tim.get("resolve_ms", 0.0), 4)
-    tmax = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    tmax = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
     if multi:
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
     tmax = float(tmax.item())
@@ -568,7 +660,7 @@ def main():
     ok = nframes if (equal == nframes and gold is not False and
                      (hand is None or (hand["checked"] == args.steps and hand["failed"] == 0))) \
         else 0
-    okt = torch.tensor([ok, nframes], dtype=torch.int64, device="cuda")
+    okt = torch.tensor([ok, nframes], dtype=torch.int64, device=cdev)
     if multi and not sharded:
         dist.all_reduce(okt)
     verified = {"frames": f"{int(okt[0])}/{int(okt[1])}",
@@ -744,8 +836,8 @@ def main():
         nonlocal group, group_err
         if group is None:
             group, group_err = join_group()
-            if group is None:
-                return {"error": f"no rc_group: {group_err}"}
+            if group is None:   # every rank agreed no group formed: no collective is pending
+                return {"group_error": f"no rc_group: {group_err}"}
         dist.barrier()
         group.render(scene, W, H, out.data_ptr(), depth=args.depth, mode=mode)   # warm
         dist.barrier()
@@ -792,7 +884,9 @@ def main():
             and group_err is None):
         shard_leg_res = run_leg_with_watchdog(shard_leg, LEG_TIMEOUT_S, leg_timed_out)
     if rank == 0:
-        if shard_leg_res:
+        if shard_leg_res and "group_error" in shard_leg_res:
+            line["group_error"] = shard_leg_res["group_error"]   # the replicas stand; exit 0
+        elif shard_leg_res:
             line["sharded_single_image"] = shard_leg_res
         print(json.dumps(line), flush=True)
     if isinstance(shard_leg_res, dict) and "error" in shard_leg_res:

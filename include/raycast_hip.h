@@ -187,7 +187,14 @@ int rc_render_device(const rc_scene *scene, int width, int height, int row0, int
  * One runs the frames' carry resolvers in submission order.  The other runs the next frame's
  * phase A and compaction and the previous frame's phase C beside it.  A frame then costs
  * about its resolver's time instead of the sum of its phases.  Fast mode (no serial stage)
- * renders the frames back to back on the whole device.  rc_frames_wait blocks until every
+ * renders the frames back to back on the whole device.
+ * Completion: rc_frames_wait is the only completion point for submitted parity frames.  The
+ * last submitted frame's phase C is held back until the next rc_frame_submit (on its lane's
+ * stream) or rc_frames_wait (on every CU), so synchronising a stream or the device after
+ * rc_frame_submit does NOT complete that frame: its DEP pixels may still hold phase A's
+ * bytes.  rc_lone_frames_check, rc_render_device and rc_render launch a pending phase C
+ * first, so a later device synchronisation completes it; rc_pipe_reset waits for it.
+ * rc_frames_wait blocks until every
  * submitted frame is complete.  It reports a failed resolver hand-off (returns -1) and fills
  * *timing (may be NULL): resolve_ms = mean resolver span; dep_pixels and zero_normalize of
  * the last frame. */
@@ -337,12 +344,6 @@ typedef struct rc_tuning {
   int headb_first;        /* one frame at a time: resolver workgroups that skip the whole-
                              workgroup queue of long regular segments and start at once on the
                              per-wave queue, whose front holds the runs that can be dense    */
-  int early_team;         /* one frame at a time: 1 = once a frame of the same scene, size and
-                             depth has shown where its long carry segments end, render those
-                             rows first and resolve their long segments (a team-only grid)
-                             while phase A of the rest of the image runs                     */
-  int band_rows;          /* test aid (with early_team): the early team's band, in rows, for
-                             every frame instead of the hint (0 = the hint)                   */
   int pipe_last_whole;    /* rc_frames_wait runs the window's last frame's phase C on every CU
                              instead of the pixel partition (1, default; 0 = the partition)   */
 } rc_tuning;

@@ -83,8 +83,6 @@ rc_tuning default_tuning() {
   // so the dense runs reach the helpers ~0.5 ms earlier and the team segment alone bounds the
   // resolver (lone quadric 4096^2 4.66 -> 4.55-4.56 ms; profiles/r05e_lone_headb.txt)
   t.headb_first = 24;
-  t.early_team = 0;
-  t.band_rows = 0;
   t.pipe_last_whole = 1;
   return t;
 }
@@ -112,7 +110,7 @@ const char* spin_site(int code) {
   return code >= 1 && code <= 4 ? site[code] : "?";
 }
 
-int FrameLog::enqueue(const void* team, hipStream_t st, long long k) {
+int FrameLog::enqueue(const void* team, hipStream_t st) {
   if (!ring) {
     HIP_TRY(hipHostMalloc((void**)&ring, kRing * sizeof(Entry), hipHostMallocDefault));
     for (int i = 0; i < kRing; ++i) ring[i].code = kPending;
@@ -123,7 +121,6 @@ int FrameLog::enqueue(const void* team, hipStream_t st, long long k) {
   }
   Entry* e = &ring[head % kRing];
   ((volatile Entry*)e)->code = kPending;
-  key[head % kRing] = k;
   HIP_TRY(hipMemcpyAsync(e, team, sizeof(Entry), hipMemcpyDeviceToHost, st));
   ++head;
   return 0;
@@ -151,10 +148,6 @@ long long FrameLog::poll() {
     if (e->clock_mhz > 0) {
       if (diag.clock_min == 0 || e->clock_mhz < diag.clock_min) diag.clock_min = e->clock_mhz;
       if (e->clock_mhz > diag.clock_max) diag.clock_max = e->clock_mhz;
-    }
-    if (code == 0) {   // a verified frame's long-segment extent: the next frame's band hint
-      hint_key = key[tail % kRing];
-      hint_row = e->team_row;
     }
     e->code = kPending;
     ++tail;
@@ -607,7 +600,7 @@ int rc_set_tuning(const rc_tuning* t) {
       in(t->block_min, 0, 1 << 30) && in(t->pipe_inres, 0, 2) && in(t->x0, 0, 1) &&
       in(t->resolve_clean, 1, 64) && in(t->shard_lone, 0, 1) && in(t->team_cscan, 0, 1) &&
       in(t->pipe_order, 0, 3) && in(t->pipe_helpers, 0, rc::kDenseSlots) &&
-      in(t->patch_host, 0, 2) && in(t->share_device, 0, 1) && in(t->headb_first, 0, 1 << 16) && in(t->early_team, 0, 1) && in(t->band_rows, 0, 1 << 30) && in(t->pipe_last_whole, 0, 1) &&
+      in(t->patch_host, 0, 2) && in(t->share_device, 0, 1) && in(t->headb_first, 0, 1 << 16) && in(t->pipe_last_whole, 0, 1) &&
       !(t->split_shade && !t->side);
   if (!ok) {
     std::fprintf(stderr, "Error: rc_set_tuning: a field is out of range\n");
@@ -899,6 +892,29 @@ int ensure_parity(DevCtx& c, FrameBufs& b, int W, int H, rc::ParityWork& w, int 
   return 0;
 }
 
+// The pending phase C (Pipe::cdefer) of the last submitted frame: on its lane's phase C
+// stream, or with `whole` on the device stream over every CU — the window's last frame, whose
+// phase C otherwise ran alone on the pixel partition after the last resolver (0.8 ms of a
+// 20-frame window's drain at quadric 4096^2 against ~0.47 ms on every CU).
+int flush_phase_c(DevCtx& c, bool whole) {
+  Pipe& p = c.pipe;
+  if (!p.cdefer) return 0;
+  p.cdefer = false;
+  rc::ParityWork& w = p.cdefer_w;
+  hipStream_t s = p.pc[p.cdefer_lane];
+  if (whole) {
+    s = c.stream;
+    w.phase_c_blocks = c.cus * 8;
+  }
+  HIP_TRY(rc::launch_phase_c(p.cdefer_ls, p.cdefer_W, p.cdefer_H, p.cdefer_maxrec, p.cdefer_out,
+                             w, p.cdefer_zc, s));
+  // the frame's hand-off words, before the event that lets slot k's next frame reset them
+  if (p.log.enqueue(w.team, s)) return -1;
+  HIP_TRY(hipEventRecord(p.cdone[p.cdefer_k], s));
+  p.cpend[p.cdefer_k] = true;
+  return 0;
+}
+
 int enqueue_render_ws(DevCtx& c, const rc_scene* s, int W, int H, int row0, int row_step,
                       int nrows, const rc_options* opt, uint8_t* d_out, hipStream_t stream,
                       bool timed, uint32_t* patch, hipEvent_t** evset);
@@ -908,6 +924,9 @@ int enqueue_render_ws(DevCtx& c, const rc_scene* s, int W, int H, int row0, int 
 int enqueue_render(DevCtx& c, const rc_scene* s, int W, int H, int row0, int row_step, int nrows,
                    const rc_options* opt, uint8_t* d_out, hipStream_t stream, bool timed,
                    uint32_t* patch, hipEvent_t** evset) {
+  // a frame in flight's held-back phase C goes out first, so that a device synchronisation
+  // after this call completes it (rc_frames_wait stays the frames' completion point)
+  if (flush_phase_c(c, false)) return -1;
   if (c.ws_valid && c.ws_stream != stream) HIP_TRY(hipStreamWaitEvent(stream, c.ws_ev, 0));
   const int rc = enqueue_render_ws(c, s, W, H, row0, row_step, nrows, opt, d_out, stream, timed,
                                    patch, evset);
@@ -961,58 +980,8 @@ int enqueue_render_ws(DevCtx& c, const rc_scene* s, int W, int H, int row0, int 
   if (maxrec < 3) w.inres = 0;
   w.patch = patch;
   w.inject = take_inject();
-  // The early team: the previous verified frame of this scene, size and depth had its long
-  // carry segments end by row `last`; this frame renders rows [0, last + 3) first and starts a
-  // team-only resolver on their list while phase A of the rest runs (launch_parity).  The band
-  // is only a schedule: the list is cut at the band's last writer, so the image is the same
-  // for any band (a long segment the band misses is resolved by the rest of the frame, and
-  // bit 30 of the frame's record then turns the hint off).
-  const rc_tuning tu = tune();
-  const long long key = ((long long)(uintptr_t)c.fb.scene_src * 1000003ll) ^
-                        ((long long)W << 40) ^ ((long long)H << 20) ^ (long long)maxrec;
-  int band = 0;
-  if (tu.early_team && w.inres && !w.side && w.team_blocks > 0 && !w.trace &&
-      c.lone_log.hint_key == key) {
-    const int hr = c.lone_log.hint_row;
-    const int last = (hr & 0x3fffffff) - 1;
-    if (!(hr & (1 << 30)) && last >= 0 && last + 3 < H * 3 / 4) band = last + 3;
-  }
-  // test aid: a forced band (any row count: the image does not depend on it)
-  if (tu.early_team && tu.band_rows > 0 && w.inres && !w.side && w.team_blocks > 0 && !w.trace)
-    band = tu.band_rows < H ? tu.band_rows : 0;
-  if (band > 0) {
-    const size_t P = (size_t)W * H;
-    if (c.fb.band.ensure(256) || c.fb.seg_start0.ensure(P * sizeof(int)) ||
-        c.fb.seg_key0.ensure(P * sizeof(long long)) ||
-        c.fb.seg_order0.ensure((size_t)rc::kSegOrderMax * sizeof(int))) {
-      std::fprintf(stderr, "Error: out of device memory for the parity workspace\n");
-      return -1;
-    }
-    if (!c.tstream) {
-      HIP_TRY(hipStreamCreateWithFlags(&c.tstream, hipStreamNonBlocking));
-      HIP_TRY(hipEventCreateWithFlags(&c.e0, hipEventDisableTiming));
-      HIP_TRY(hipEventCreateWithFlags(&c.et, hipEventDisableTiming));
-    }
-    w.band_rows = band;
-    w.team_grid = w.team_blocks;     // the early team: its own grid, one workgroup per CU
-    w.team_blocks = 0;               // the rest of the frame has no team of its own
-    w.resolve_blocks -= w.team_grid; // and runs on the CUs the early team leaves
-    if (w.helpers > w.resolve_blocks / 2) w.helpers = w.resolve_blocks / 2;
-    if (w.headb_first > w.resolve_blocks - w.helpers) w.headb_first = w.resolve_blocks - w.helpers;
-    w.counters0 = (int*)c.fb.band.p;
-    w.pcut = (long long*)((char*)c.fb.band.p + 128);
-    w.seg_start0 = (int*)c.fb.seg_start0.p;
-    w.seg_key0 = (long long*)c.fb.seg_key0.p;
-    w.seg_order0 = (int*)c.fb.seg_order0.p;
-    w.tstream = c.tstream;
-    w.e0 = c.e0;
-    w.et = c.et;
-    c.lone_band = band;
-  } else {
-    c.lone_band = 0;
-  }
   HIP_TRY(rc::launch_parity(ls, W, H, maxrec, d_out, w, zc, stream, timed ? ev + 1 : nullptr));
-  return c.lone_log.enqueue(w.team, stream, key);
+  return c.lone_log.enqueue(w.team, stream);
 }
 
 // After a synchronised parity render: the resolver's and phase C's bounded spins set
@@ -1301,6 +1270,7 @@ void pipe_release(DevCtx& c) {
     (void)hipEventDestroy(e[1]);
   }
   p.init = false;
+  p.cdefer = false;   // nothing launched stays pending across a rebuilt pipeline
   p.submitted = 0;
   p.frames = 0;
   p.last = -1;
@@ -1318,29 +1288,6 @@ void pipe_release(DevCtx& c) {
 
 void pipe_release_all() {
   for (auto& c : g_ctx) pipe_release(c);
-}
-
-// The pending phase C (Pipe::cdefer) of the last submitted frame: on its lane's phase C
-// stream, or with `whole` on the device stream over every CU — the window's last frame, whose
-// phase C otherwise ran alone on the pixel partition after the last resolver (0.8 ms of a
-// 20-frame window's drain at quadric 4096^2 against ~0.47 ms on every CU).
-int flush_phase_c(DevCtx& c, bool whole) {
-  Pipe& p = c.pipe;
-  if (!p.cdefer) return 0;
-  p.cdefer = false;
-  rc::ParityWork& w = p.cdefer_w;
-  hipStream_t s = p.pc[p.cdefer_lane];
-  if (whole) {
-    s = c.stream;
-    w.phase_c_blocks = c.cus * 8;
-  }
-  HIP_TRY(rc::launch_phase_c(p.cdefer_ls, p.cdefer_W, p.cdefer_H, p.cdefer_maxrec, p.cdefer_out,
-                             w, p.cdefer_zc, s));
-  // the frame's hand-off words, before the event that lets slot k's next frame reset them
-  if (p.log.enqueue(w.team, s)) return -1;
-  HIP_TRY(hipEventRecord(p.cdone[p.cdefer_k], s));
-  p.cpend[p.cdefer_k] = true;
-  return 0;
 }
 
 int pipe_init(DevCtx& c, long long pixels) {
@@ -1629,6 +1576,7 @@ int rc_lone_frames_check(int64_t* checked, int64_t* failed) {
   // the lock first: a frame another thread enqueues after the synchronisation would otherwise
   // be drained while still pending (counted as never verified)
   std::lock_guard<std::mutex> lk(c->mu);
+  if (flush_phase_c(*c, false)) return -1;   // a frame in flight's held-back phase C
   HIP_TRY(hipDeviceSynchronize());   // the frames ran on the callers' streams
   c->lone_log.drain();
   long long ch = 0, f = 0;

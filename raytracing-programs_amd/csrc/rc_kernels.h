@@ -79,20 +79,6 @@ struct ParityWork {
                             // their own work is done (rc_tuning.side 3)
   int block_min;            // regular segments of >= block_min entries get a whole workgroup
   int headb_first;          // regular workgroups that start on the per-wave queue (head B) at once
-  // Early team (one frame at a time, launch_parity): band_rows > 0 = phase A and a DEP list of
-  // rows [0, band_rows) first, cut at the band's last writer; a team-only resolver grid
-  // (team_grid workgroups, on tstream) resolves that list's long segments while phase A of the
-  // rest, the whole image's list and this frame's resolver (no team of its own: its long
-  // segments below band 0's DEP count are the early team's) run on the main stream.
-  int band_rows;
-  int team_grid;
-  int* counters0;           // band 0's counters (nseg, ndep, ...)
-  int* seg_start0;          // band 0's segment table and order
-  long long* seg_key0;
-  int* seg_order0;
-  long long* pcut;          // band 0's cut pixel (k_band_cut)
-  hipStream_t tstream;
-  hipEvent_t e0, et;        // band 0's list is ready / the early team is done
 };
 
 constexpr int kSegOrderMax = 65536;   // segments ordered for the resolver queue (else FIFO)

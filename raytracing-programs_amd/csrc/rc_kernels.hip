@@ -438,7 +438,7 @@ __device__ __forceinline__ void stage_row_chunk(const uint8_t* __restrict__ src,
   }
 }
 
-// The one-workgroup kernels of the compaction (k_row_scan, k_seg_order, k_band_cut) run as
+// The one-workgroup kernels of the compaction (k_row_scan, k_seg_order) run as
 // kScanBlock threads.  With frames in flight they are dispatched beside the next frame's
 // phase A, whose workgroups (4 waves of 128 VGPRs) refill every CU slot they free: a
 // 1024-thread workgroup needs a whole CU's wave slots at once and waited 0.05-1.2 ms for one
@@ -710,18 +710,15 @@ __device__ __forceinline__ void seg_order_body(const int* __restrict__ seg_start
   if (t == 0) counters[3] = 1;
 }
 
-// plim (optional, the early team's band 0): pixels at or after *plim count as class ident
 __global__ void __launch_bounds__(256) k_row_compact(
     const uint8_t* __restrict__ cls, int W, int H, const int* __restrict__ row_off,
     const int* __restrict__ row_soff, const long long* __restrict__ row_prevw,
     const long long* __restrict__ row_prevd, long long* __restrict__ dep_pix,
-    int* __restrict__ seg_start, long long* __restrict__ seg_key,
-    const long long* __restrict__ plim = nullptr) {
+    int* __restrict__ seg_start, long long* __restrict__ seg_key) {
   __shared__ __attribute__((aligned(16))) uint8_t s_row[kRowWaves][kRowChunk];
   const int wave = threadIdx.x >> 6;
   const int y = blockIdx.x * kRowWaves + wave;
-  const long long lim = plim ? *plim : 0x7fffffffffffffffll;
-  const bool on = y < H && (long long)y * W < lim;
+  const bool on = y < H;
   const int lane = threadIdx.x & 63;
   const long long base = (long long)y * W;
   const unsigned long long lt = lanemask_lt();
@@ -734,7 +731,7 @@ __global__ void __launch_bounds__(256) k_row_compact(
 #pragma unroll 8
     for (int x0 = xc; x0 < (on ? xc + n : xc); x0 += 64) {
       const int x = x0 + lane;
-      const uint8_t c = (x < W && base + x < lim) ? s_row[wave][x - xc] : kClsIdent;
+      const uint8_t c = x < W ? s_row[wave][x - xc] : kClsIdent;
       const unsigned long long md = __ballot(c == kClsDep), mw = __ballot(c == kClsWriter);
       if (md) {
         const long long kw = (mw & lt) ? base + x0 + hi_bit(mw & lt) : lw;
@@ -759,56 +756,6 @@ __global__ void __launch_bounds__(256) k_row_compact(
     }
     __syncthreads();   // the chunk buffer is refilled
   }
-}
-
-// The early team's band 0 (rows [0, R0), launch_parity): its DEP list ends at the band's last
-// writer p (a segment never crosses a writer, so every segment before p is whole and every
-// later one starts at p or after it, in band 1).  After k_row_stats over the band's rows: p,
-// the stats of p's row recomputed as if every pixel at or after p were class ident, the rows
-// after it emptied, and *pcut = p (0 when the band has no writer: an empty band-0 list).
-// One workgroup of kScanBlock.
-__global__ void __launch_bounds__(kScanBlock) k_band_cut(const uint8_t* __restrict__ cls, int W,
-                                                   int R0, RowStats* __restrict__ rs,
-                                                   long long* __restrict__ pcut) {
-  __shared__ unsigned long long s_p;
-  if (threadIdx.x == 0) s_p = 0;
-  __syncthreads();
-  long long m = -1;
-  for (int y = threadIdx.x; y < R0; y += blockDim.x) m = rs[y].lastw > m ? rs[y].lastw : m;
-  if (m >= 0) atomicMax(&s_p, (unsigned long long)m + 1);
-  __syncthreads();
-  const long long p = (long long)s_p - 1;   // -1: no writer in the band
-  const int rc = p >= 0 ? (int)(p / W) : -1;
-  for (int y = rc + 1 + (int)threadIdx.x; y < R0; y += blockDim.x)
-    rs[y] = RowStats{0, 0, -1, -1, -1};
-  if (p >= 0 && threadIdx.x < 64) {   // wave 0: row rc below p
-    const int lane = threadIdx.x;
-    const long long base = (long long)rc * W;
-    const unsigned long long lt = lanemask_lt();
-    int nd = 0, ns = 0;
-    long long lw = -1, ld = -1, wf = -1;
-    for (int x0 = 0; x0 < W; x0 += 64) {
-      const int x = x0 + lane;
-      const uint8_t c = (x < W && base + x < p) ? cls[base + x] : kClsIdent;
-      const unsigned long long md = __ballot(c == kClsDep), mw = __ballot(c == kClsWriter);
-      if (md) {
-        const long long kw = (mw & lt) ? base + x0 + hi_bit(mw & lt) : lw;
-        const long long pd = (md & lt) ? base + x0 + hi_bit(md & lt) : ld;
-        const bool st = c == kClsDep && pd >= 0 && kw > pd;
-        ns += __popcll(__ballot(st));
-        if (wf < 0 && ld < 0) {
-          const int f = __ffsll((long long)md) - 1;
-          const unsigned long long wb = mw & ((f ? (~0ull >> (64 - f)) : 0ull));
-          wf = wb ? base + x0 + hi_bit(wb) : lw;
-        }
-        nd += __popcll(md);
-        ld = base + x0 + hi_bit(md);
-      }
-      if (mw) lw = base + x0 + hi_bit(mw);
-    }
-    if (lane == 0) rs[rc] = RowStats{nd, ns, lw, ld, wf};
-  }
-  if (threadIdx.x == 0) *pcut = p >= 0 ? p : 0;
 }
 
 // ------------------------------------------------------------ parity phase B: carry --
@@ -1959,12 +1906,7 @@ __global__ void __launch_bounds__(kResolveBlock) __attribute__((amdgpu_waves_per
     int helpers, int hand_run, int inject, int block_min, int headb_first,
     int* __restrict__ rq_cnt,
     int* __restrict__ rq, Cam cam, int W, uint8_t* __restrict__ out, uint32_t* __restrict__ patch,
-    unsigned long long* __restrict__ zcount, int* __restrict__ batch_state, int inres,
-    int team_only, const int* __restrict__ ext_n0, const int* __restrict__ full_ndep) {
-  // team_only (the early team, launch_parity): this grid is a team over band 0's list and
-  // nothing else; full_ndep = the whole image's DEP count (0 until its compaction has run).
-  // ext_n0 (the rest of an early-team frame): band 0's DEP count — long segments that start
-  // below it are the early team's.
+    unsigned long long* __restrict__ zcount, int* __restrict__ batch_state, int inres) {
   if (!RC_X0_RESOLVE) sc.has_quadric = sc.has_quadric != 0;   // no cross-term-free form here (RC_X0_*)
   // the product build has no trace: its timestamps and counters then hold no registers
   if (!RC_DIAG) trace = nullptr;
@@ -1979,7 +1921,6 @@ __global__ void __launch_bounds__(kResolveBlock) __attribute__((amdgpu_waves_per
   const int nseg = counters[0];
   const int ndep = counters[2];
   const bool ordered = counters[3] != 0;
-  const int n0e = ext_n0 ? *ext_n0 : 0;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   // The chain steps read the winner's record (hit_frame) and refl[obj] every bounce level:
   // stage the shape records (n <= kLdsShapes) in LDS so those reads cost an LDS access
@@ -2032,20 +1973,7 @@ __global__ void __launch_bounds__(kResolveBlock) __attribute__((amdgpu_waves_per
     const int cE = 64 / cGE;
     const bool cscan_on = RC_TEAM_CSCAN && team_cscan && G > 0 && 2 * G <= 64;
     int round = 0;
-    // the early team shares its CUs with phase A of band 1: the leader's waves (its RESOLVE
-    // rounds are the frame's serial chain) issue first on their SIMDs
-    if (team_only && blockIdx.x == 0) __builtin_amdgcn_s_setprio(3);
-    // team_only: batches of 64 entries below band 0's last whole one are credited as usual;
-    // the last, partial one also holds band-1 entries, so its size needs the whole image's
-    // count — its band-0 part is credited once the team is done and that count is known
-    const int cut = team_only ? (ndep & ~63) : 0x7fffffff;
-    int held0 = 0x7fffffff, held1 = 0;
     auto credit = [&](int j0, int j1) {   // the crediter wave (all its lanes)
-      if (j1 > cut) {
-        held0 = min(held0, max(j0, cut));
-        held1 = max(held1, j1);
-        j1 = cut;
-      }
       ready_range(rq_cnt, rq, ts, ndep, j0, j1);
     };
     // the long segments lead the length-ordered queue (k_seg_order): stop at the first
@@ -2329,7 +2257,7 @@ __global__ void __launch_bounds__(kResolveBlock) __attribute__((amdgpu_waves_per
         ts->n_scan += n_scan_;
         ts->n_cscan += n_cscan_;
         ts->n_resolve += n_resolve_;
-        // the next frame's band hint: the last row this long segment reaches
+        // diagnostic: the last row a long segment reaches (FrameLog)
         atomicMax(&ts->team_row, (int)(dep_pix[end - 1] / W) + 1);
       }
       if (trace && blockIdx.x == 0 && threadIdx.x == 0) {
@@ -2338,26 +2266,6 @@ __global__ void __launch_bounds__(kResolveBlock) __attribute__((amdgpu_waves_per
         trace[3 * s + 2] = (unsigned)(__builtin_amdgcn_s_memtime() - c_seg);
         trace[3 * (size_t)ndep + 4 * (size_t)nseg + 8 * 8192 + s] = (unsigned)t_seg;
       }
-    }
-    if (team_only) {   // the early team leaves: the rest of the frame is another grid's
-      if ((int)blockIdx.x == T - 1 && wave == 0 && held0 < held1) {
-        int nf = 0;
-        if (lane == 0) {
-          const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-          while ((nf = __hip_atomic_load(full_ndep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) <
-                 ndep) {
-            if (spin_expired(ts, t0)) {
-              set_error(ts, 2, held0, held1);
-              nf = -1;
-              break;
-            }
-            __builtin_amdgcn_s_sleep(8);
-          }
-        }
-        nf = __shfl(nf, 0, 64);
-        if (nf >= ndep) ready_range(rq_cnt, rq, ts, nf, held0, held1);
-      }
-      return;
     }
     // the team's segments are done: its waves join the regular queue (every wave from here
     // on is independent; a frame without long segments gets the whole grid)
@@ -2495,10 +2403,7 @@ __global__ void __launch_bounds__(kResolveBlock) __attribute__((amdgpu_waves_per
       const int sg = ordered ? seg_order[q] : q;
       const int start = seg_start[sg];
       const int end = (sg + 1 < nseg) ? seg_start[sg + 1] : ndep;
-      if (end - start >= long_len) {
-        if (team_blocks > 0 || start < n0e) continue;   // the team's, or the early team's
-        if (ext_n0 && t == 0) atomicOr(&ts->team_row, 1 << 30);   // band 0 missed it
-      }
+      if (end - start >= long_len && team_blocks > 0) continue;   // the team's
       const unsigned long long t_seg = __builtin_amdgcn_s_memrealtime();
       const unsigned long long c_seg = __builtin_amdgcn_s_memtime();
       V3 c = seg_init_carry(seg_key, wcarry, sg);
@@ -2568,10 +2473,7 @@ __global__ void __launch_bounds__(kResolveBlock) __attribute__((amdgpu_waves_per
     if (ordered) s = seg_order[s];
     const int start = seg_start[s];
     const int end = (s + 1 < nseg) ? seg_start[s + 1] : ndep;
-    if (end - start >= long_len) {
-      if (team_blocks > 0 || start < n0e) continue;   // the team's, or the early team's
-      if (ext_n0 && lane == 0) atomicOr(&ts->team_row, 1 << 30);   // band 0 missed it
-    }
+    if (end - start >= long_len && team_blocks > 0) continue;   // the team's
     const unsigned long long t_seg = __builtin_amdgcn_s_memrealtime();
     const unsigned long long c_seg = __builtin_amdgcn_s_memtime();
     int iters = 0;
@@ -3106,76 +3008,6 @@ hipError_t launch_parity(const LaunchScene& s, int W, int H, int maxrec, uint8_t
   const bool st = stage_fits(s);
   dim3 grid((W + kTileW - 1) / kTileW, (H + kTileH - 1) / kTileH);
   auto kres = s.n <= kLdsShapes ? k_resolve<true> : k_resolve<false>;
-  if (w.band_rows > 0 && w.band_rows < H && !w.side && !w.rstream) {   // the early team
-    const int R0 = w.band_rows;
-    // the whole image's counters first: the early team reads their DEP count (0 until set)
-    (void)hipMemsetAsync(w.counters, 0, 16 * sizeof(int), stream);
-    dim3 g0((W + kTileW - 1) / kTileW, (R0 + kTileH - 1) / kTileH);
-    hipLaunchKernelGGL(st ? k_phase_a<true> : k_phase_a<false>, g0, dim3(kBlock), 0, stream, sc,
-                       cam, W, 0, 1, R0, maxrec, out, w.cls, w.wcarry, (DepLine*)w.deprec,
-                       zcount, W);
-    // band 0's list; k_row_stats also clears the frame's TeamState and phase C's batch arrays
-    const int rb0 = (R0 + kRowWaves - 1) / kRowWaves;
-    hipLaunchKernelGGL(k_row_stats, dim3(rb0), dim3(256), 0, stream, w.cls, W, R0,
-                       (RowStats*)w.row_stats, w.counters0, (uint4*)w.team,
-                       (int)(sizeof(TeamState) / sizeof(uint4)), w.batch_state, w.batch_ints);
-    hipLaunchKernelGGL(k_band_cut, dim3(1), dim3(kScanBlock), 0, stream, w.cls, W, R0,
-                       (RowStats*)w.row_stats, w.pcut);
-    hipLaunchKernelGGL(k_row_scan, dim3(1), dim3(kScanBlock), 0, stream, R0,
-                       (const RowStats*)w.row_stats, w.row_off, w.row_soff, w.row_prevw,
-                       w.row_prevd, w.counters0);
-    hipLaunchKernelGGL(k_row_compact, dim3(rb0), dim3(256), 0, stream, w.cls, W, R0, w.row_off,
-                       w.row_soff, w.row_prevw, w.row_prevd, w.dep_pix, w.seg_start0, w.seg_key0,
-                       (const long long*)w.pcut);
-    hipLaunchKernelGGL(k_seg_order, dim3(1), dim3(kScanBlock), 0, stream, w.seg_start0, w.counters0,
-                       w.seg_order0, w.batch_state, w.batch_cnt, w.batch_rq, 0, 0, 0);
-    (void)hipEventRecord(w.e0, stream);
-    (void)hipStreamWaitEvent(w.tstream, w.e0, 0);
-    hipLaunchKernelGGL(kres, dim3(w.team_grid), dim3(kResolveBlock), w.resolve_lds, w.tstream,
-                       sc, maxrec, (const DepLine*)w.deprec, w.dep_pix, w.seg_key0, w.wcarry,
-                       w.seg_start0, w.seg_order0, w.counters0, w.counters0 + 1, (CinG*)w.cin,
-                       w.team_grid, w.long_len, (TeamState*)w.team, (unsigned*)nullptr,
-                       w.coop_group, w.wave_k, w.resolve_k,
-                       w.resolve_clean > 0 ? w.resolve_clean : 1, w.team_cscan, w.epoch, 0,
-                       w.hand_run, 0, 0, 0, w.inres ? w.batch_cnt : nullptr, w.batch_rq, cam, W,
-                       out, w.patch, zcount, w.batch_state, 0, 1, (const int*)nullptr,
-                       (const int*)(w.counters + 2));
-    (void)hipEventRecord(w.et, w.tstream);
-    // band 1 beside the early team, then the whole image's list
-    const size_t off = (size_t)R0 * W;
-    dim3 g1((W + kTileW - 1) / kTileW, (H - R0 + kTileH - 1) / kTileH);
-    hipLaunchKernelGGL(st ? k_phase_a<true> : k_phase_a<false>, g1, dim3(kBlock), 0, stream, sc,
-                       cam, W, R0, 1, H - R0, maxrec, out + off * 3, w.cls + off, w.wcarry + off,
-                       (DepLine*)w.deprec + off, zcount, W);
-    if (ev) (void)hipEventRecord(ev[0], stream);
-    const int row_blocks = (H + kRowWaves - 1) / kRowWaves;
-    hipLaunchKernelGGL(k_row_stats, dim3(row_blocks), dim3(256), 0, stream, w.cls, W, H,
-                       (RowStats*)w.row_stats, w.counters, (uint4*)nullptr, 0, (int*)nullptr, 0);
-    hipLaunchKernelGGL(k_row_scan, dim3(1), dim3(kScanBlock), 0, stream, H,
-                       (const RowStats*)w.row_stats, w.row_off, w.row_soff, w.row_prevw,
-                       w.row_prevd, w.counters);
-    hipLaunchKernelGGL(k_row_compact, dim3(row_blocks), dim3(256), 0, stream, w.cls, W, H,
-                       w.row_off, w.row_soff, w.row_prevw, w.row_prevd, w.dep_pix, w.seg_start,
-                       w.seg_key, (const long long*)nullptr);
-    hipLaunchKernelGGL(k_seg_order, dim3(1), dim3(kScanBlock), 0, stream, w.seg_start, w.counters,
-                       w.seg_order, w.batch_state, w.batch_cnt, w.batch_rq, w.block_min,
-                       w.resolve_blocks - w.team_blocks - w.helpers - w.headb_first, 0);
-    if (ev) (void)hipEventRecord(ev[1], stream);
-    hipLaunchKernelGGL(kres, dim3(w.resolve_blocks), dim3(kResolveBlock), w.resolve_lds, stream,
-                       sc, maxrec, (const DepLine*)w.deprec, w.dep_pix, w.seg_key, w.wcarry,
-                       w.seg_start, w.seg_order, w.counters, w.counters + 1, (CinG*)w.cin,
-                       w.team_blocks, w.long_len, (TeamState*)w.team, w.trace, w.coop_group,
-                       w.wave_k, w.resolve_k, w.resolve_clean > 0 ? w.resolve_clean : 1,
-                       w.team_cscan, w.epoch, w.helpers, w.hand_run, w.inject, w.block_min,
-                       w.headb_first, w.inres ? w.batch_cnt : nullptr, w.batch_rq, cam, W, out,
-                       w.patch, zcount, w.batch_state, w.inres, 0, (const int*)(w.counters0 + 2),
-                       (const int*)nullptr);
-    (void)hipStreamWaitEvent(stream, w.et, 0);
-    if (ev) (void)hipEventRecord(ev[2], stream);
-    enqueue_phase_c(sc, cam, st, W, H, maxrec, out, w, zcount, stream);
-    if (ev) (void)hipEventRecord(ev[3], stream);
-    return hipGetLastError();
-  }
   if (w.side && w.split_shade)   // carry part only; colours shaded beside the resolver (k_side)
     hipLaunchKernelGGL(st ? k_classify<true> : k_classify<false>, grid, dim3(kBlock), 0, stream, sc, cam, W, H, maxrec, w.cls,
                        w.wcarry, (DepLine*)w.deprec);
@@ -3223,8 +3055,7 @@ hipError_t launch_parity(const LaunchScene& s, int W, int H, int maxrec, uint8_t
                      w.long_len, (TeamState*)w.team, w.trace, w.coop_group, w.wave_k,
                      w.resolve_k, w.resolve_clean > 0 ? w.resolve_clean : 1, w.team_cscan, w.epoch, w.helpers, w.hand_run, w.inject, w.block_min,
                      w.headb_first, (w.side || w.inres) ? w.batch_cnt : nullptr, w.batch_rq, cam, W, out,
-                     w.patch, zcount, w.batch_state, w.inres, 0, (const int*)nullptr,
-                     (const int*)nullptr);
+                     w.patch, zcount, w.batch_state, w.inres);
   if (w.rstream) {
     if (w.rt1) (void)hipEventRecord(w.rt1, rs);
     (void)hipEventRecord(w.rdone, rs);
@@ -3421,7 +3252,7 @@ hipError_t launch_shard_resolve(const LaunchScene& s, int W, int H, int G, int r
                      w.wave_k, w.resolve_k, w.resolve_clean > 0 ? w.resolve_clean : 1,
                      w.team_cscan, w.epoch, w.helpers, w.hand_run, w.inject, w.block_min,
                      w.headb_first, w.inres ? w.batch_cnt : nullptr, w.batch_rq, cam, W, out, (uint32_t*)nullptr,
-                     zcount, w.batch_state, w.inres, 0, (const int*)nullptr, (const int*)nullptr);
+                     zcount, w.batch_state, w.inres);
   if (ev) (void)hipEventRecord(ev[1], stream);
   enqueue_phase_c(sc, cam, stage_fits(s), W, H, maxrec, out, w, zcount, stream);
   return hipGetLastError();

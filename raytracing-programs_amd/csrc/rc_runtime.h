@@ -49,9 +49,6 @@ struct FrameBufs {
   const void* scene_src = nullptr;   // host image last uploaded
   DevBuf cls, wcarry, deprec, rows, dep_pix, seg_key, seg_start, seg_order, batch_state, cin,
       counters, team, trace;
-  // the early team's band 0 (one frame at a time): its counters and cut pixel, segment table
-  // and order (allocated at the first early-team frame)
-  DevBuf band, seg_start0, seg_key0, seg_order0;
 };
 
 // Per-frame verification of parity frames.  A frame's carry hand-offs (the resolver team's
@@ -71,7 +68,7 @@ struct FrameLog {
     int n_scan, n_cscan, n_resolve; // the frame's team rounds by kind
     int spin_ticks[4];              // its longest bounded waits per spin site (10 ns ticks)
     int clock_mhz;                  // shader clock over its resolver's run (0: not measured)
-    int team_row;                   // TeamState::team_row: 1 + last row of a long segment, bit 30
+    int team_row;                   // TeamState::team_row: 1 + last row of a long segment
   };
   // Frame diagnostics of the entries read back since the last diag_take(): frames, the most
   // team rounds of each kind in one frame, the longest wait per spin site.
@@ -83,17 +80,13 @@ struct FrameLog {
   };
   Diag diag;
   Entry* ring = nullptr;     // pinned host memory, kRing entries
-  long long key[kRing] = {}; // the schedule key each logged frame was enqueued with
-  // the newest frame read back: its key and team_row (the early team's band hint)
-  long long hint_key = -1;
-  int hint_row = 0;
   long long head = 0;        // frames logged
   long long tail = 0;        // frames whose entry has been read back (in order)
   long long checked = 0;     // entries read back since the last take()
   long long failed = 0;      // of them, frames whose hand-off failed
   const char* what = "";
   // Log the frame whose TeamState is `team` (device) on `st`, after its last kernel.
-  int enqueue(const void* team, hipStream_t st, long long k = -1);
+  int enqueue(const void* team, hipStream_t st);
   // Read back the entries whose copy has run (in order, stopping at the first still
   // pending); reports each failure on stderr.  Returns the failures found.
   long long poll();
@@ -196,9 +189,6 @@ struct DevCtx {
   // rc_render's overlapped copy (parity): the framebuffer leaves on `d2h` while the resolver
   // runs, then only the DEP entries' colours (`patch`, packed RGB per entry) follow
   hipStream_t d2h = nullptr;
-  // the early team's stream and events (launch_parity band_rows)
-  hipStream_t tstream = nullptr;
-  hipEvent_t e0 = nullptr, et = nullptr;
   DevBuf patch;
   uint8_t* pin_pix = nullptr;     // pinned: DEP pixel indices (int64 per entry)
   uint8_t* pin_patch = nullptr;   // pinned: DEP entries' packed RGB
@@ -214,7 +204,6 @@ struct DevCtx {
   // resolver placement of the last frame of each kind (grid, CUs it may use)
   rc_resolver_stats pipe_stats{};
   int lone_grid = 0, lone_res_cus = 0, lone_lds = 0, lone_team = 0;
-  int lone_band = 0;   // the last lone frame's early-team band (rows; 0: none)
   int pipe_grid = 0, pipe_res_cus = 0, pipe_lds = 0, pipe_team = 0;
   // `fb` is shared by every one-frame-at-a-time call on this device, and rc_render_device
   // returns before its frame has run: the next enqueue on `fb` from another stream waits for

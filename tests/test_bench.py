@@ -59,3 +59,80 @@ def test_golden_lookup():
     assert bench.golden_md5("quadric", 4096, 4096, 6, "parity") == "3bf1c59fc7cf7e508e5b1796348e9726"
     assert bench.golden_md5("quadric", 4096, 4096, 6, "fast") == "7b6a08a014498b1c3b81df44fce9b776"
     assert bench.golden_md5("quadric", 123, 4096, 6, "parity") is None
+
+
+# ---- bench.py --gpus N without a launcher ----
+
+def test_resolve_world():
+    assert bench.resolve_world(None, {}) == (1, False)
+    assert bench.resolve_world(1, {}) == (1, False)
+    assert bench.resolve_world(8, {}) == (8, True)          # self-launch 8 ranks
+    assert bench.resolve_world(None, {"WORLD_SIZE": "4"}) == (4, False)
+    assert bench.resolve_world(4, {"WORLD_SIZE": "4"}) == (4, False)   # the driver's torchrun
+    for gpus, env in ((8, {"WORLD_SIZE": "2"}), (1, {"WORLD_SIZE": "2"}), (0, {})):
+        try:
+            bench.resolve_world(gpus, env)
+        except ValueError:
+            continue
+        raise AssertionError((gpus, env))
+
+
+def test_launch_plan_argv_and_env():
+    env = {"PATH": "/usr/bin", "HSA_ENABLE_IPC_MODE_LEGACY": "0", "RC_BENCH_BACKEND": "gloo"}
+    argv = ["--gpus", "4", "--steps", "5"]
+    plans = bench.launch_plan(4, argv, env, 29999)
+    assert len(plans) == 4
+    for r, (a, e) in enumerate(plans):
+        assert a[0] == sys.executable and a[-4:] == argv
+        assert os.path.samefile(a[a.index("-u") + 1], os.path.join(ROOT, "bench.py"))
+        assert (e["RANK"], e["LOCAL_RANK"], e["WORLD_SIZE"]) == (str(r), str(r), "4")
+        assert (e["MASTER_ADDR"], e["MASTER_PORT"]) == ("127.0.0.1", "29999")
+        # the caller's environment travels (IPC mode, rehearsal backend)
+        assert e["HSA_ENABLE_IPC_MODE_LEGACY"] == "0" and e["RC_BENCH_BACKEND"] == "gloo"
+    assert "RANK" not in env   # the parent's own environment is untouched
+
+
+def test_worst_status():
+    assert bench.worst_status([0, 0, 0]) == 0
+    assert bench.worst_status([0, 3, 0]) == 3
+    assert bench.worst_status([4, 3]) == 4
+    assert bench.worst_status([0, -9]) == 137   # killed by SIGKILL
+    assert bench.worst_status([]) == 0
+
+
+def _py(code):
+    return [sys.executable, "-c", code]
+
+
+def test_run_ranks_relays_codes_and_kills_stuck_ranks():
+    env = dict(os.environ)
+    assert bench.run_ranks([(_py("pass"), env), (_py("import sys; sys.exit(0)"), env)]) == [0, 0]
+    # one rank fails, the other is stuck (as in a collective with the dead rank): killed after
+    # the grace period by its own PID
+    import time
+    t0 = time.monotonic()
+    codes = bench.run_ranks([(_py("import sys; sys.exit(4)"), env),
+                             (_py("import time; time.sleep(600)"), env)], grace_s=1.0)
+    assert codes[0] == 4 and codes[1] == -9, codes
+    assert time.monotonic() - t0 < 30
+    assert bench.worst_status(codes) == 137
+
+
+def test_self_launch_end_to_end_without_gpu():
+    """`bench.py --gpus 2` with no launcher starts two ranks; here (no GPU) each rank stops
+    with its own message before any GPU call and the parent exits with their status."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "RC_BENCH_BACKEND")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
+                        "--steps", "1", "--warmup", "0"], capture_output=True, text=True,
+                       env=env, timeout=300)
+    assert r.returncode == 2, (r.returncode, r.stderr[-2000:])
+    assert "rank 0 needs GPU 0" in r.stderr and "rank 1 needs GPU 1" in r.stderr, r.stderr
+    assert "rank exit codes [2, 2]" in r.stderr
+
+
+def test_gpus_must_match_the_launcher():
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8"],
+                       capture_output=True, text=True, env=env, timeout=120)
+    assert r.returncode == 2 and "--gpus 8 but the launcher started WORLD_SIZE=2" in r.stderr

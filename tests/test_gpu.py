@@ -75,8 +75,7 @@ SCHEDULES = {"no-side": dict(side=0), "side-always": dict(side=1), "side-by-size
              "device-patch": dict(patch_host=0),
              "mapped-patch-after-frame": dict(patch_host=1),
              "helpers-8-hand-run-512": dict(helpers=8, hand_run=512),
-             "no-headb-first": dict(headb_first=0), "early-team": dict(early_team=1),
-             "early-band-300": dict(early_team=1, band_rows=300)}
+             "no-headb-first": dict(headb_first=0)}
 
 
 @pytest.mark.parametrize("sched", list(SCHEDULES))
@@ -776,40 +775,34 @@ def test_resolver_diagnostics_record(scenes, table):
     assert p3_md5(out.cpu().numpy()) == want
 
 
-@pytest.mark.parametrize("key", ["quadric:4096x4096:d6:parity", "simple:1024x1024:d6:parity",
-                                 "reflection:2048x2048:d4:parity", "quadric:1024x1024:d6:parity",
-                                 "quadric:8192x8192:d6:parity", "quadric:333x517:d6:parity"])
-def test_early_team(key, scenes, table):
-    """Lone frames with the early team (rc_tuning.early_team): the first frame of a scene, size
-    and depth records where its long carry segments end; the next ones render those rows first
-    and resolve their long segments on a team-only grid while phase A of the rest runs (the
-    band's list cut at its last writer).  Every frame md5-equal to the reference, through the
-    drop-in path (rc_render) and device-resident (rc_render_device), and every hand-off
-    verified."""
+def test_held_back_phase_c_completion_points(scenes, table):
+    """the last submitted frame's phase C is held back until the next submit or
+    rc_frames_wait.  rc_lone_frames_check and a lone render launch it first, so a device
+    synchronisation after them completes every submitted frame; rc_frames_wait still verifies
+    the window afterwards, and rc_pipe_reset leaves nothing pending."""
     torch = pytest.importorskip("torch")
-    scene, size, d, mode = key.split(":")
-    w, h = map(int, size.split("x"))
+    n, key = 1024, "quadric:1024x1024:d6:parity"
     want = table[key]["md5"]
-    with rc.tuned(early_team=1):
-        for i in range(3):
-            assert p3_md5(rc.render(scenes[scene], w, h, depth=int(d[1:]), mode=mode)) == want, i
-        out = torch.empty((h, w, 3), dtype=torch.uint8, device="cuda")
-        for i in range(2):
-            rc.render_device(scenes[scene], w, h, out.data_ptr(), depth=int(d[1:]), mode=mode)
-            torch.cuda.synchronize()
-            assert p3_md5(out.cpu().numpy()) == want, ("device", i)
-    chk = rc.lone_frames_check()
-    assert chk["failed"] == 0
-
-
-@pytest.mark.parametrize("band", [1, 100, 161, 204, 369, 370, 512, 1023])
-def test_early_team_forced_bands(band, scenes, table):
-    """Forced early-team bands (rc_tuning.band_rows) anywhere in simple 1024^2 d6, whose 88k-entry
-    long segment runs over rows 161-369: a band that ends inside it (204: the cut that broke
-    round 3's two-band attempt) leaves the segment to the rest of the frame, which resolves it
-    with a whole workgroup; the image is the same for every band."""
-    key = "simple:1024x1024:d6:parity"
-    with rc.tuned(early_team=1, band_rows=band):
-        for i in range(2):
-            assert p3_md5(rc.render(scenes["simple"], 1024, 1024, depth=6)) == table[key]["md5"], i
+    s = scenes["quadric"]
+    rc.frames_wait()
+    bufs = [torch.zeros((n, n, 3), dtype=torch.uint8, device="cuda") for _ in range(3)]
+    torch.cuda.synchronize()
+    for b in bufs[:2]:
+        rc.frame_submit(s, n, n, b.data_ptr(), depth=6)
+    rc.lone_frames_check()   # launches frame 1's held-back phase C
+    torch.cuda.synchronize()
+    assert [p3_md5(b.cpu().numpy()) for b in bufs[:2]] == [want] * 2
+    rc.frame_submit(s, n, n, bufs[2].data_ptr(), depth=6)
+    out = torch.empty((n, n, 3), dtype=torch.uint8, device="cuda")
+    rc.render_device(s, n, n, out.data_ptr(), depth=6)   # a lone render flushes it too
+    torch.cuda.synchronize()
+    assert p3_md5(bufs[2].cpu().numpy()) == want and p3_md5(out.cpu().numpy()) == want
+    tim = {}
+    rc.frames_wait(tim)
+    assert (tim["frames_checked"], tim["frames_failed"]) == (3, 0)
+    rc.frame_submit(s, n, n, bufs[0].data_ptr(), depth=6)
+    rc.pipe_reset()   # waits for the window, then rebuilds the pipeline on the next submit
+    rc.frame_submit(s, n, n, bufs[1].data_ptr(), depth=6)
+    rc.frames_wait(tim)
+    assert (tim["frames_checked"], tim["frames_failed"]) == (1, 0)
     assert rc.lone_frames_check()["failed"] == 0
