@@ -7,8 +7,9 @@
 // costs the team leader, evaluator and step overhead together.
 //
 //   hipcc <the product flags> -Iinclude -Iraytracing-programs_amd/csrc scripts/block_bench.hip
-//   /tmp/block_bench entries.bin [windows] [variant]
+//   /tmp/block_bench entries.bin [windows] [variant: 0 product step, 2 split by shape class]
 #include "../raytracing-programs_amd/csrc/rc_kernels.hip"
+#include "split_step.hpp"
 
 #include <cstdio>
 #include <cstring>
@@ -42,6 +43,8 @@ __global__ void __launch_bounds__(kResolveBlock) k_bb(Scene sc, const BEntry* __
   ls.has = kself < sc.n;
   ls.s = sc.shapes[ls.has ? kself : sc.n];
   __shared__ BlockWinShared bw;
+  __shared__ SplitX sxs[2];                                       // variant 2: the split step
+  const SplitLane sl = split_lane(sc, threadIdx.x >> 6, lane);
   unsigned long long cyc = 0, steps = 0, chg = 0;
   for (int wi = 0; wi < nwin; ++wi) {
     const int j = wstart[wi];
@@ -59,7 +62,10 @@ __global__ void __launch_bounds__(kResolveBlock) k_bb(Scene sc, const BEntry* __
       block_window_lean(sc, 7, bw, j, nv, c, ls, G, dense, changed, 64, cin, tag, ws);
     else
 #endif
-      block_window(sc, 7, bw, j, nv, c, ls, G, dense, changed, 64, cin, tag, ws, nullptr, false);
+      if (variant == 2)
+        split_block_window(sc, 7, bw, sxs, sl, j, nv, c, cin, tag, ws);
+      else
+        block_window(sc, 7, bw, j, nv, c, ls, G, dense, changed, 64, cin, tag, ws, nullptr, false);
     const unsigned long long t1 = __builtin_amdgcn_s_memtime();
     cyc += t1 - t0;
     steps += ws.coop + ws.lane;
