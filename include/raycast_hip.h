@@ -328,7 +328,9 @@ typedef struct rc_tuning {
                              resolvers, pixel streams, phase C; 2 pixel streams, phase C,
                              resolvers; 3 each resolver lane on a hardware queue of its own
                              (placeholder streams fill the others; needs two lanes and the
-                             default stream layout, else order 2 with a warning)          */
+                             default stream layout, else order 2 with a warning); 4 one phase
+                             C stream for both lanes and each resolver lane beside an idle
+                             placeholder (same conditions as 3)                           */
   int pipe_helpers;       /* frames in flight: dense-run helper workgroups per resolver lane
                              (default 4; 0 = none)                                            */
   int patch_host;         /* rc_render (parity, overlap_d2h): phase C writes the DEP entries'

@@ -599,7 +599,7 @@ int rc_set_tuning(const rc_tuning* t) {
       in(t->comp_stream, 0, 2) && in(t->side_blocks, 0, 1 << 16) &&
       in(t->block_min, 0, 1 << 30) && in(t->pipe_inres, 0, 2) && in(t->x0, 0, 1) &&
       in(t->resolve_clean, 1, 64) && in(t->shard_lone, 0, 1) && in(t->team_cscan, 0, 1) &&
-      in(t->pipe_order, 0, 3) && in(t->pipe_helpers, 0, rc::kDenseSlots) &&
+      in(t->pipe_order, 0, 4) && in(t->pipe_helpers, 0, rc::kDenseSlots) &&
       in(t->patch_host, 0, 2) && in(t->share_device, 0, 1) && in(t->headb_first, 0, 1 << 16) && in(t->pipe_last_whole, 0, 1) &&
       !(t->split_shade && !t->side);
   if (!ok) {
@@ -1263,8 +1263,9 @@ void pipe_release(DevCtx& c) {
   for (int r = 0; r < p.lanes; ++r) {
     (void)hipStreamDestroy(p.res[r]);
     if (r < 2 && p.comp[r]) (void)hipStreamDestroy(p.comp[r]);
-    if (p.pc[r]) (void)hipStreamDestroy(p.pc[r]);
+    if (p.pc[r] && (r == 0 || !p.pc_shared)) (void)hipStreamDestroy(p.pc[r]);
   }
+  p.pc_shared = false;
   for (auto& e : p.rt) {
     (void)hipEventDestroy(e[0]);
     (void)hipEventDestroy(e[1]);
@@ -1373,11 +1374,26 @@ int pipe_init(DevCtx& c, long long pixels) {
       HIP_TRY(hipExtStreamCreateWithCUMask(&p.spare[r], (uint32_t)words, ma.data()));
     HIP_TRY(hipExtStreamCreateWithCUMask(&p.pix[1], (uint32_t)words, mb.data()));
     HIP_TRY(hipExtStreamCreateWithCUMask(&p.pc[1], (uint32_t)words, mb.data()));
+  } else if (tu.pipe_order == 4 && p.fifo && p.lanes == 2) {
+    // one phase C stream for both lanes (consecutive frames' phase C never overlap: a lane's
+    // resolver ends half a frame period after the other's), so with the device stream created
+    // first and four hardware queues dealt in creation order each resolver lane shares its
+    // queue only with an idle placeholder: {device stream, pix[0]}, {res[0], spare},
+    // {res[1], spare}, {pc, pix[1]}
+    for (int r = 0; r < 2; ++r)
+      HIP_TRY(hipExtStreamCreateWithCUMask(&p.res[r], (uint32_t)words, ma.data()));
+    HIP_TRY(hipExtStreamCreateWithCUMask(&p.pc[0], (uint32_t)words, mb.data()));
+    p.pc[1] = p.pc[0];
+    p.pc_shared = true;
+    HIP_TRY(hipExtStreamCreateWithCUMask(&p.pix[0], (uint32_t)words, mb.data()));
+    for (int r = 0; r < 2; ++r)
+      HIP_TRY(hipExtStreamCreateWithCUMask(&p.spare[r], (uint32_t)words, ma.data()));
+    HIP_TRY(hipExtStreamCreateWithCUMask(&p.pix[1], (uint32_t)words, mb.data()));
   } else {
-    if (tu.pipe_order == 3)
-      std::fprintf(stderr, "Warning: pipe_order 3 needs two resolver lanes and the default "
+    if (tu.pipe_order >= 3)
+      std::fprintf(stderr, "Warning: pipe_order %d needs two resolver lanes and the default "
                    "stream layout (pipe_resolvers %d, pipe_slotstreams %d): using order 2\n",
-                   p.lanes, p.fifo ? 0 : 1);
+                   tu.pipe_order, p.lanes, p.fifo ? 0 : 1);
     if (mk_pix() || mk_pc() || mk_res()) return -1;
   }
   for (int k = 0; k < p.slots; ++k) {

@@ -134,7 +134,8 @@ struct Pipe {
   hipEvent_t ready[kSlots] = {}, done[kSlots] = {};
   bool fifo = true;                  // pa = pix[0] + pc[] (false: RC_PIPE_SLOTSTREAMS)
   hipStream_t pc[kLanes] = {};
-  hipStream_t spare[2] = {};         // pipe_order 3: placeholders that keep a queue per lane
+  hipStream_t spare[2] = {};         // pipe_order 3/4: placeholders that keep a queue per lane
+  bool pc_shared = false;            // pipe_order 4: both lanes' phase C on one stream (pc[0])
   hipEvent_t cdone[kSlots] = {};
   bool cpend[kSlots] = {};           // slot k's phase C is enqueued and not yet synchronised
   hipEvent_t adone[kSlots] = {};     // after slot k's phase A

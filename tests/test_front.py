@@ -220,7 +220,7 @@ def test_tuning_api_validates():
     for bad in (dict(pipe_resolvers=0), dict(pipe_resolvers=5), dict(helpers=65),
                 dict(team_blocks=-2), dict(resolve_grid=4), dict(split_shade=1, side=0),
                 dict(copy_threads=0), dict(resolve_lds_kb=200), dict(long_len=10), dict(x0=2),
-                dict(pipe_order=4), dict(patch_host=3), dict(share_device=2),
+                dict(pipe_order=5), dict(patch_host=3), dict(share_device=2),
                 dict(headb_first=-1), dict(pipe_last_whole=2)):
         with pytest.raises(ValueError):
             rc.set_tuning(**bad)

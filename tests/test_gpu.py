@@ -297,6 +297,7 @@ PIPES = {"default": {},
          "lane-helpers-every-run": dict(pipe_helpers=8, hand_run=2),
          "stream-order-1": dict(pipe_order=1),
          "queue-per-lane": dict(pipe_order=3),
+         "one-phase-c-stream": dict(pipe_order=4),
          "last-phase-c-on-partition": dict(pipe_last_whole=0)}
 
 
