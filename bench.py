@@ -77,31 +77,27 @@ def load_pkg():
     return mod
 
 
-# rocprofv3 --pmc summaries of this exact configuration from HEAD (scripts/pmc_valu.sh,
-# scripts/pmc_fast.sh -> scripts/pmc_summary.py): per-kernel counter means per launch.
-PMC_PROFILES = {("quadric", 4096, 6, "parity"): "profiles/r05fl_pmc_lone_4096.json",
-                ("reflection", 2048, 4, "parity"): "profiles/r03e_pmc_lone_c3.json",
-                ("quadric", 8192, 6, "parity"): "profiles/r03e_pmc_lone_c5.json",
-                ("quadric", 4096, 6, "fast"): "profiles/r02c_pmc_fast_4096.json"}
+# rocprofv3 --pmc summaries of this exact configuration at HEAD, all from one call of
+# scripts/pmc_all.sh (kernel stats, VALU/wave-state and FETCH/WRITE passes per configuration ->
+# scripts/pmc_summary.py): per-kernel counter means per launch.  Lone frames for parity (the
+# one-frame-at-a-time schedule, phase C inside the resolver), the timed launches for fast mode.
+PMC_PROFILES = {("quadric", 4096, 6, "parity"): "profiles/r06g_pmc_c4.json",
+                ("reflection", 2048, 4, "parity"): "profiles/r06g_pmc_c3.json",
+                ("quadric", 8192, 6, "parity"): "profiles/r06g_pmc_c5.json",
+                ("quadric", 4096, 6, "fast"): "profiles/r06g_pmc_fast.json"}
 
-
-# FETCH/WRITE of the frames-in-flight launches themselves (scripts/pmc_traffic.py over the
-# bench's timed launches): a pipeline lane's resolver has no phase C inside, so its traffic
-# differs from the lone frame's
-PMC_TRAFFIC_INFLIGHT = {("quadric", 4096, 6, "parity"): "profiles/r03f_pmc_traffic_inflight_4096.json"}
-
-# The headline's whole counter set from ONE command at HEAD (scripts/pmc_headline.sh: kernel
-# stats, VALU/wave-state and FETCH/WRITE passes of `bench.py --timed-only --steps 20 --warmup
-# 3`, the default frames in flight): valu_busy and traffic of the headline line come from it.
-PMC_HEADLINE = {("quadric", 4096, 6, "parity"): "profiles/r05f_pmc_headline.json"}
+# The headline's whole counter set from the same call, on the driver's command itself
+# (`bench.py --timed-only --steps 20 --warmup 5`, frames in flight): valu_busy and traffic of
+# the headline line's dominant kernel come from the launches it times.
+PMC_HEADLINE = {("quadric", 4096, 6, "parity"): "profiles/r06g_pmc_headline.json"}
 
 
 def pmc_kernel(kernel, scene, size, depth, mode, inflight=False):
     """Counter means of `kernel` from the committed PMC summary of this configuration:
     hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 per launch (the gfx950 correction of
     MI355X_MICROARCH.md), write_bytes = WRITE_SIZE * 1024, valu_busy; (None, None) when no
-    profile covers it.  inflight: hbm_bytes from the frames-in-flight traffic summary when one
-    exists (valu_busy stays the lone frame's)."""
+    profile covers it.  inflight: every figure from the frames-in-flight summary of the
+    driver's command when one exists (PMC_HEADLINE)."""
     def find(rel):
         if not rel or not os.path.exists(os.path.join(ROOT, rel)):
             return None
@@ -126,11 +122,6 @@ def pmc_kernel(kernel, scene, size, depth, mode, inflight=False):
                     "write_bytes": h["WRITE_SIZE"] * 1024 if "WRITE_SIZE" in h else None,
                     "valu_busy": h.get("valu_busy"),
                     "frac_wait_any": h.get("frac_wait_any")}, hrel
-        trel = PMC_TRAFFIC_INFLIGHT.get((scene, size, depth, mode))
-        t = find(trel)
-        if t is not None:
-            out["hbm_bytes"] = t.get("hbm_bytes")
-            rel = f"{trel} (traffic); {rel} (valu_busy, lone frame)"
     return out, rel
 
 

@@ -136,3 +136,19 @@ def test_gpus_must_match_the_launcher():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8"],
                        capture_output=True, text=True, env=env, timeout=120)
     assert r.returncode == 2 and "--gpus 8 but the launcher started WORLD_SIZE=2" in r.stderr
+
+
+def test_counter_files_exist_and_are_current():
+    """every counter summary bench.py reads exists, is this round's (one
+    scripts/pmc_all.sh call at HEAD) and covers the line's dominant kernel."""
+    import json
+    maps = list(bench.PMC_PROFILES.items()) + list(bench.PMC_HEADLINE.items())
+    assert maps
+    for (scene, size, depth, mode), rel in maps:
+        assert os.path.basename(rel).startswith("r06g_"), rel
+        with open(os.path.join(ROOT, rel)) as f:
+            ks = {k.split("::")[-1].split("<")[0] for k in json.load(f)["kernels"]}
+        want = "k_render" if mode == "fast" else "k_resolve"
+        assert want in ks, (rel, ks)
+    pmc, src = bench.pmc_kernel("k_resolve", "quadric", 4096, 6, "parity", inflight=True)
+    assert src == bench.PMC_HEADLINE[("quadric", 4096, 6, "parity")] and pmc["hbm_bytes"] > 0
