@@ -348,14 +348,6 @@ typedef struct rc_tuning {
                              per-wave queue, whose front holds the runs that can be dense    */
   int pipe_last_whole;    /* rc_frames_wait runs the window's last frame's phase C on every CU
                              instead of the pixel partition (1, default; 0 = the partition)   */
-  int lead_rows;          /* one frame at a time: the early leader's band — phase A and the DEP
-                             list of the first lead_rows rows first, then one workgroup on a
-                             CU of its own resolves the band's last segment while phase A of
-                             the other rows runs; the team resumes it (-1 = H/32, default; 0 =
-                             off)                                                             */
-  int pipe_lead;          /* frames in flight: the early leader per frame (band H/32), on one
-                             CU per resolver lane taken from the pixel partition; it works
-                             until the lane is free for the frame's resolver (0 off)           */
 } rc_tuning;
 void rc_default_tuning(rc_tuning *t);
 int rc_set_tuning(const rc_tuning *t);

@@ -118,8 +118,7 @@ TUNING_FIELDS = ["side", "split_shade", "resolve_shared", "resolve_lds_kb", "res
                  "staged_d2h", "prefault", "copy_threads", "side_blocks", "comp_stream",
                  "block_min", "pipe_inres", "x0", "resolve_clean",
                  "shard_lone", "team_cscan", "pipe_order", "pipe_helpers", "patch_host",
-                 "share_device", "headb_first", "pipe_last_whole",
-                 "lead_rows", "pipe_lead"]
+                 "share_device", "headb_first", "pipe_last_whole"]
 
 
 class RcTuning(ctypes.Structure):

@@ -84,8 +84,6 @@ rc_tuning default_tuning() {
   // resolver (lone quadric 4096^2 4.66 -> 4.55-4.56 ms; profiles/r05e_lone_headb.txt)
   t.headb_first = 24;
   t.pipe_last_whole = 1;
-  t.lead_rows = -1;
-  t.pipe_lead = 0;
   return t;
 }
 rc_tuning g_tune = default_tuning();
@@ -602,7 +600,7 @@ int rc_set_tuning(const rc_tuning* t) {
       in(t->block_min, 0, 1 << 30) && in(t->pipe_inres, 0, 2) && in(t->x0, 0, 1) &&
       in(t->resolve_clean, 1, 64) && in(t->shard_lone, 0, 1) && in(t->team_cscan, 0, 1) &&
       in(t->pipe_order, 0, 4) && in(t->pipe_helpers, 0, rc::kDenseSlots) &&
-      in(t->patch_host, 0, 2) && in(t->share_device, 0, 1) && in(t->headb_first, 0, 1 << 16) && in(t->pipe_last_whole, 0, 1) && in(t->lead_rows, -1, 1 << 20) && in(t->pipe_lead, 0, 1) &&
+      in(t->patch_host, 0, 2) && in(t->share_device, 0, 1) && in(t->headb_first, 0, 1 << 16) && in(t->pipe_last_whole, 0, 1) &&
       !(t->split_shade && !t->side);
   if (!ok) {
     std::fprintf(stderr, "Error: rc_set_tuning: a field is out of range\n");
@@ -618,8 +616,7 @@ int rc_set_tuning(const rc_tuning* t) {
     if (!c.pipe.init) continue;
     if (t->pipe_resolvers != c.pipe.built_lanes || t->pipe_slots != c.pipe.built_slots ||
         t->pipe_res_cus != c.pipe.built_res || (t->pipe_timing != 0) != c.pipe.rt_on ||
-        (t->pipe_slotstreams == 0) != c.pipe.fifo || t->pipe_order != c.pipe.built_order ||
-        (t->pipe_lead != 0) != c.pipe.lead) {
+        (t->pipe_slotstreams == 0) != c.pipe.fifo || t->pipe_order != c.pipe.built_order) {
       std::fprintf(stderr, "Warning: rc_set_tuning: the pipe_* fields take effect when device "
                    "%d's frame pipeline is rebuilt (rc_pipe_reset)\n", c.device);
       break;
@@ -921,7 +918,6 @@ int flush_phase_c(DevCtx& c, bool whole) {
 int enqueue_render_ws(DevCtx& c, const rc_scene* s, int W, int H, int row0, int row_step,
                       int nrows, const rc_options* opt, uint8_t* d_out, hipStream_t stream,
                       bool timed, uint32_t* patch, hipEvent_t** evset);
-void register_release();
 
 // Enqueue one render of rows (row0 + k*row_step) into d_out on `stream`, using the device's
 // one-frame workspace c.fb: after the previous render that used it, whatever its stream.
@@ -984,38 +980,6 @@ int enqueue_render_ws(DevCtx& c, const rc_scene* s, int W, int H, int row0, int 
   if (maxrec < 3) w.inres = 0;
   w.patch = patch;
   w.inject = take_inject();
-  // the early leader (rc_kernels.hip k_lead): a band of the first H/32 rows (-1, the default)
-  // or lead_rows rows; lone frames with phase C inside the resolver and a team
-  const int lr = tune().lead_rows;
-  const int lead = lr < 0 ? H / 32 : lr;
-  if (lead > 0 && lead < H && w.inres && !w.side && w.team_blocks > 0 && maxrec >= 3) {
-    const size_t n0 = (size_t)lead * W;
-    if (c.fb.lead.ensure(128) || c.fb.lead_pix.ensure(n0 * sizeof(long long)) ||
-        c.fb.lead_seg.ensure(n0 * (sizeof(long long) + sizeof(int)))) {
-      std::fprintf(stderr, "Error: out of device memory for the parity workspace\n");
-      return -1;
-    }
-    if (!c.lstream) {   // CU masks: the leader on the device's last CU, the rest elsewhere
-      register_release();
-      const int words = (c.cus + 31) / 32;
-      std::vector<uint32_t> ml(words, 0), mr(words, 0);
-      for (int i = 0; i < c.cus; ++i) (i == c.cus - 1 ? ml : mr)[i / 32] |= 1u << (i % 32);
-      HIP_TRY(hipExtStreamCreateWithCUMask(&c.lstream, (uint32_t)words, ml.data()));
-      HIP_TRY(hipExtStreamCreateWithCUMask(&c.pstream2, (uint32_t)words, mr.data()));
-      for (auto& e : c.le) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    }
-    w.lead_rows = lead;
-    w.lead_counters = (int*)c.fb.lead.p;
-    w.lead_pre = (int*)((char*)c.fb.lead.p + 64);
-    w.lead_dep_pix = (long long*)c.fb.lead_pix.p;
-    w.lead_seg_key = (long long*)c.fb.lead_seg.p;
-    w.lead_seg_start = (int*)((char*)c.fb.lead_seg.p + n0 * sizeof(long long));
-    w.lstream = c.lstream;
-    w.pstream2 = c.pstream2;
-    w.le0 = c.le[0];
-    w.le1 = c.le[1];
-    w.le2 = c.le[2];
-  }
   HIP_TRY(rc::launch_parity(ls, W, H, maxrec, d_out, w, zc, stream, timed ? ev + 1 : nullptr));
   return c.lone_log.enqueue(w.team, stream);
 }
@@ -1295,15 +1259,7 @@ void pipe_release(DevCtx& c) {
     (void)hipEventDestroy(p.done[k]);
     (void)hipEventDestroy(p.cdone[k]);
     (void)hipEventDestroy(p.adone[k]);
-    if (p.lead0[k]) (void)hipEventDestroy(p.lead0[k]);
-    if (p.lead1[k]) (void)hipEventDestroy(p.lead1[k]);
-    p.lead0[k] = p.lead1[k] = nullptr;
   }
-  for (auto& l : p.lstream) {
-    if (l) (void)hipStreamDestroy(l);
-    l = nullptr;
-  }
-  p.lead = false;
   for (int r = 0; r < p.lanes; ++r) {
     (void)hipStreamDestroy(p.res[r]);
     if (r < 2 && p.comp[r]) (void)hipStreamDestroy(p.comp[r]);
@@ -1332,24 +1288,17 @@ void pipe_release(DevCtx& c) {
 }
 
 void pipe_release_all() {
-  for (auto& c : g_ctx) {
-    pipe_release(c);
-    if (c.lstream) {   // the early leader's CU-masked streams, like the pipeline's
-      (void)hipSetDevice(c.device);
-      (void)hipDeviceSynchronize();
-      (void)hipStreamDestroy(c.lstream);
-      (void)hipStreamDestroy(c.pstream2);
-      for (auto& e : c.le) (void)hipEventDestroy(e);
-      c.lstream = c.pstream2 = nullptr;
-    }
-  }
+  for (auto& c : g_ctx) pipe_release(c);
 }
-
 
 int pipe_init(DevCtx& c, long long pixels) {
   Pipe& p = c.pipe;
   if (p.init) return 0;
-  register_release();
+  static bool registered = false;
+  if (!registered) {
+    std::atexit(pipe_release_all);
+    registered = true;
+  }
   // partition A: the low `res` bits of the CU mask, which the driver deals round-robin over
   // the XCDs (bit i -> XCD i mod 8), so both partitions span every XCD.
   // Resolver partition by image size, fixed at the first pipelined frame (measured with frames
@@ -1374,17 +1323,6 @@ int pipe_init(DevCtx& c, long long pixels) {
   const int words = (c.cus + 31) / 32;
   std::vector<uint32_t> ma(words, 0), mb(words, 0);
   for (int i = 0; i < c.cus; ++i) (i < res ? ma : mb)[i / 32] |= 1u << (i % 32);
-  // the early leader (pipe_lead): the pixel partition's last CU per lane, one stream each
-  p.lead = tu.pipe_lead != 0 && p.fifo && p.lanes <= 2;
-  if (p.lead) {
-    for (int r = 0; r < p.lanes; ++r) {
-      const int cu = c.cus - 1 - r;
-      mb[cu / 32] &= ~(1u << (cu % 32));
-      std::vector<uint32_t> ml(words, 0);
-      ml[cu / 32] |= 1u << (cu % 32);
-      HIP_TRY(hipExtStreamCreateWithCUMask(&p.lstream[r], (uint32_t)words, ml.data()));
-    }
-  }
   // the CU-masked streams, in the order tu.pipe_order names (the runtime assigns hardware
   // queues in creation order, and a queue's dispatcher serves one kernel's workgroups at a time)
   const bool comp = tu.comp_stream == 1 || (tu.comp_stream == 2 && pixels >= (32ll << 20));
@@ -1459,10 +1397,6 @@ int pipe_init(DevCtx& c, long long pixels) {
     if (mk_pix() || mk_pc() || mk_res()) return -1;
   }
   for (int k = 0; k < p.slots; ++k) {
-    if (p.lead) {
-      HIP_TRY(hipEventCreateWithFlags(&p.lead0[k], hipEventDisableTiming));
-      HIP_TRY(hipEventCreateWithFlags(&p.lead1[k], hipEventDisableTiming));
-    }
     HIP_TRY(hipEventCreateWithFlags(&p.adone[k], hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&p.ready[k], hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&p.done[k], hipEventDisableTiming));
@@ -1482,14 +1416,6 @@ int pipe_init(DevCtx& c, long long pixels) {
 }
 
 }  // namespace
-
-namespace rcrt {
-// the CU-masked streams (frame pipeline, early leader) go before the runtime's own teardown
-void register_release() {
-  static std::atomic<bool> registered{false};
-  if (!registered.exchange(true)) std::atexit(pipe_release_all);
-}
-}  // namespace rcrt
 
 extern "C" {
 
@@ -1554,24 +1480,6 @@ int rc_frame_submit(const rc_scene* s, int W, int H, const rc_options* opt, uint
   w.rt0 = p.rt_on ? p.rt[e][0] : nullptr;
   w.rt1 = p.rt_on ? p.rt[e][1] : nullptr;
   w.inject = take_inject();
-  const int lead = H / 32;   // the early leader's band (pipe_lead), as for lone frames
-  if (p.lead && lead > 0 && maxrec >= 3 && w.team_blocks > 0) {
-    const size_t n0 = (size_t)lead * W;
-    if (b.lead.ensure(128) || b.lead_pix.ensure(n0 * sizeof(long long)) ||
-        b.lead_seg.ensure(n0 * (sizeof(long long) + sizeof(int)))) {
-      std::fprintf(stderr, "Error: out of device memory for the parity workspace\n");
-      return -1;
-    }
-    w.lead_rows = lead;
-    w.lead_counters = (int*)b.lead.p;
-    w.lead_pre = (int*)((char*)b.lead.p + 64);
-    w.lead_dep_pix = (long long*)b.lead_pix.p;
-    w.lead_seg_key = (long long*)b.lead_seg.p;
-    w.lead_seg_start = (int*)((char*)b.lead_seg.p + n0 * sizeof(long long));
-    w.lstream = p.lstream[lane];
-    w.le0 = p.lead0[k];
-    w.le1 = p.lead1[k];
-  }
   HIP_TRY(rc::launch_parity(ls, W, H, maxrec, d_out, w, zc, st, nullptr));
   if (p.fifo) {   // phase C after the resolver: at the next submit or rc_frames_wait
     p.cdefer = true;

@@ -79,21 +79,6 @@ struct ParityWork {
                             // their own work is done (rc_tuning.side 3)
   int block_min;            // regular segments of >= block_min entries get a whole workgroup
   int headb_first;          // regular workgroups that start on the per-wave queue (head B) at once
-  // Early leader (one frame at a time, launch_parity; lead_rows > 0): phase A and the DEP list
-  // of rows [0, lead_rows) first; one workgroup (k_lead, alone on the CU of lstream's mask)
-  // resolves the band's last segment from its start while phase A of the other rows runs on
-  // pstream2 (every other CU); it stops at the band's end or once *lead_stop is set (after the
-  // frame's compaction) and leaves {segment start + 1, position, carry} in lead_pre, where the
-  // team of k_resolve resumes the segment.
-  int lead_rows;
-  int* lead_counters;       // [16] the band's counters (nseg, -, ndep)
-  long long* lead_dep_pix;  // [lead_rows * W] the band's DEP list (the frame list's prefix)
-  int* lead_seg_start;      // [lead_rows * W] the band's segment table
-  long long* lead_seg_key;
-  int* lead_pre;            // [8] {start + 1 (0: none), position, carry x, y, z bits, -, stop, -}
-  hipStream_t lstream;      // CU mask: the leader's CU
-  hipStream_t pstream2;     // CU mask: every other CU (phase A of rows >= lead_rows)
-  hipEvent_t le0, le1, le2; // band listed / leader done / phase A of the rest done
 };
 
 constexpr int kSegOrderMax = 65536;   // segments ordered for the resolver queue (else FIFO)

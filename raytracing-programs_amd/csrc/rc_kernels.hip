@@ -1906,8 +1906,7 @@ __global__ void __launch_bounds__(kResolveBlock) __attribute__((amdgpu_waves_per
     int helpers, int hand_run, int inject, int block_min, int headb_first,
     int* __restrict__ rq_cnt,
     int* __restrict__ rq, Cam cam, int W, uint8_t* __restrict__ out, uint32_t* __restrict__ patch,
-    unsigned long long* __restrict__ zcount, int* __restrict__ batch_state, int inres,
-    const int* __restrict__ lead_pre) {
+    unsigned long long* __restrict__ zcount, int* __restrict__ batch_state, int inres) {
   if (!RC_X0_RESOLVE) sc.has_quadric = sc.has_quadric != 0;   // no cross-term-free form here (RC_X0_*)
   // the product build has no trace: its timestamps and counters then hold no registers
   if (!RC_DIAG) trace = nullptr;
@@ -1996,13 +1995,6 @@ __global__ void __launch_bounds__(kResolveBlock) __attribute__((amdgpu_waves_per
       V3 c = seg_init_carry(seg_key, wcarry, s);
       int j = start;
       bool resolve = false;
-      // the early leader (k_lead) resolved this segment's first entries during phase A: their
-      // carry-ins are published; resume at its position with its carry (a SCAN round first)
-      if (lead_pre && lead_pre[0] == start + 1) {
-        j = lead_pre[1];
-        c = v3(__int_as_float(lead_pre[2]), __int_as_float(lead_pre[3]),
-               __int_as_float(lead_pre[4]));
-      }
       int n_scan_ = 0, n_cscan_ = 0, n_resolve_ = 0;   // this segment's rounds by kind
       // the next SCAN round is cooperative (after a RESOLVE round that handed back early)
       bool cscan = false;
@@ -2015,10 +2007,6 @@ __global__ void __launch_bounds__(kResolveBlock) __attribute__((amdgpu_waves_per
       // wait instead of delaying the block's own round)
       int pend0 = 0, pend1 = 0;
       const bool crediter = (int)blockIdx.x == T - 1 && wave == 0;
-      if (j > start) {   // the early leader's entries: credited during the first round's wait
-        pend0 = start;
-        pend1 = j;
-      }
       while (j < end) {
         ++round;
         ++rounds_here;
@@ -2963,80 +2951,6 @@ __global__ void __launch_bounds__(256) k_deinterleave(const uint8_t* __restrict_
   }
 }
 
-// The early leader (launch_parity, ParityWork::lead_rows).  A lone frame's resolver cannot
-// start before the whole image's phase A and compaction (~0.83 ms at quadric 4096^2), and its
-// critical chain is the team segment, whose first ~0.45 ms are RESOLVE rounds of the team
-// leader alone: one workgroup resolving the first clusters changer by changer.  Those rounds
-// need only the segment's first entries, which lie in the image's first rows.  So phase A and
-// the DEP list of rows [0, lead_rows) come first, and this one workgroup, alone on a CU that
-// the rest of phase A (a CU-masked stream) does not use, runs the band's last segment with
-// block windows while phase A of the other rows runs.  The DEP list of a band of leading rows
-// is a prefix of the frame's list (scan order), so its indices, segment starts and carry-ins
-// are the frame's.  It stops at the band's end or at the first window after the frame's
-// compaction has raised lead_pre[6] (one window, ~5-20 us), and leaves {segment start + 1,
-// position, carry} in lead_pre; k_resolve's team resumes that segment there.  A segment the
-// frame's resolver does not give to the team is simply resolved again (identical carry-ins).
-template <bool kLds>
-__global__ void __launch_bounds__(kResolveBlock) __attribute__((amdgpu_waves_per_eu(2))) k_lead(
-    Scene sc, int maxrec, const DepLine* __restrict__ deprec,
-    const long long* __restrict__ dep_pix0, const long long* __restrict__ seg_key0,
-    const float4* __restrict__ wcarry, const int* __restrict__ seg_start0,
-    const int* __restrict__ counters0, CinG* __restrict__ cin, unsigned tag, int G, int wave_k,
-    int long_min, int* __restrict__ pre) {
-  if (!RC_X0_RESOLVE) sc.has_quadric = sc.has_quadric != 0;   // k_resolve's evaluator form
-  const int nseg = counters0[0], ndep = counters0[2];
-  const int t = threadIdx.x, lane = t & 63;
-  __shared__ rc_shape s_shapes[kLds ? kLdsShapes + 1 : 1];
-  if (kLds) {
-    const int words = (int)(sizeof(rc_shape) / 4) * (sc.n + 1);
-    for (int i = t; i < words; i += blockDim.x)
-      ((unsigned*)s_shapes)[i] = ((const unsigned*)sc.shapes)[i];
-    __syncthreads();
-    if (!RC_RES_GLOBAL_SCAN) sc.shapes = s_shapes;
-    sc.lshapes = s_shapes;
-  }
-  if (nseg <= 0) return;
-  const int s = nseg - 1;
-  const int start = seg_start0[s];
-  if (ndep - start < long_min) return;   // too short to be the team's
-  LaneShape ls;
-  ls.has = false;
-  if (G > 0) {
-    const int kself = lane % G;
-    ls.has = kself < sc.n;
-    if (ls.has) ls.s = sc.shapes[kself];
-  }
-  __shared__ BlockWinShared s_bw;
-  __shared__ int s_stop;
-  V3 c = seg_init_carry(seg_key0, wcarry, s);
-  int j = start;
-  bool dense = false;
-  WinStats ws = {0, 0, 0};
-  if (j + t < ndep) s_bw.rec[t] = rec_at(deprec, dep_pix0, j + t);
-  __syncthreads();
-  while (j < ndep) {
-    const int nv = ndep - j < kResolveBlock ? ndep - j : kResolveBlock;
-    DepRec nxt;
-    const int jn = j + nv;
-    if (jn + t < ndep) nxt = rec_at(deprec, dep_pix0, jn + t);
-    bool changed;
-    block_window(sc, maxrec, s_bw, j, nv, c, ls, G, dense, changed, wave_k, cin, tag, ws);
-    j = jn;
-    if (t == 0) s_stop = __hip_atomic_load(&pre[6], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();   // everyone is done reading this window's records; the stop flag is read
-    if (s_stop) break;
-    if (j + t < ndep) s_bw.rec[t] = nxt;
-    __syncthreads();
-  }
-  if (t == 0) {   // the carry-ins above were stored before this (in order, same workgroup)
-    pre[1] = j;
-    pre[2] = __float_as_int(c.x);
-    pre[3] = __float_as_int(c.y);
-    pre[4] = __float_as_int(c.z);
-    __hip_atomic_store(&pre[0], start + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
 // ---------------------------------------------------------------------- launchers --
 static Scene make_scene(const LaunchScene& s) {
   Scene sc;
@@ -3094,119 +3008,10 @@ hipError_t launch_parity(const LaunchScene& s, int W, int H, int maxrec, uint8_t
   const bool st = stage_fits(s);
   dim3 grid((W + kTileW - 1) / kTileW, (H + kTileH - 1) / kTileH);
   auto kres = s.n <= kLdsShapes ? k_resolve<true> : k_resolve<false>;
-  if (w.lead_rows > 0 && w.lead_rows < H && !w.side && !w.rstream && w.team_blocks > 0) {
-    // the early leader (k_lead): band 0's phase A and list, then the leader on its own CU
-    // beside phase A of the other rows (pstream2), then the frame's list and resolver
-    const int R0 = w.lead_rows;
-    (void)hipMemsetAsync(w.lead_counters, 0, 16 * sizeof(int), stream);
-    (void)hipMemsetAsync(w.lead_pre, 0, 8 * sizeof(int), stream);
-    dim3 g0((W + kTileW - 1) / kTileW, (R0 + kTileH - 1) / kTileH);
-    hipLaunchKernelGGL(st ? k_phase_a<true> : k_phase_a<false>, g0, dim3(kBlock), 0, stream, sc,
-                       cam, W, 0, 1, R0, maxrec, out, w.cls, w.wcarry, (DepLine*)w.deprec,
-                       zcount, W);
-    (void)hipEventRecord(w.le0, stream);
-    (void)hipStreamWaitEvent(w.pstream2, w.le0, 0);
-    const size_t off = (size_t)R0 * W;
-    dim3 g1((W + kTileW - 1) / kTileW, (H - R0 + kTileH - 1) / kTileH);
-    hipLaunchKernelGGL(st ? k_phase_a<true> : k_phase_a<false>, g1, dim3(kBlock), 0, w.pstream2,
-                       sc, cam, W, R0, 1, H - R0, maxrec, out + off * 3, w.cls + off,
-                       w.wcarry + off, (DepLine*)w.deprec + off, zcount, W);
-    (void)hipEventRecord(w.le2, w.pstream2);
-    // band 0's list (its own tables: the frame's compaction rewrites the shared ones)
-    const int rb0 = (R0 + kRowWaves - 1) / kRowWaves;
-    hipLaunchKernelGGL(k_row_stats, dim3(rb0), dim3(256), 0, stream, w.cls, W, R0,
-                       (RowStats*)w.row_stats, w.lead_counters, (uint4*)nullptr, 0, (int*)nullptr,
-                       0);
-    hipLaunchKernelGGL(k_row_scan, dim3(1), dim3(kScanBlock), 0, stream, R0,
-                       (const RowStats*)w.row_stats, w.row_off, w.row_soff, w.row_prevw,
-                       w.row_prevd, w.lead_counters);
-    hipLaunchKernelGGL(k_row_compact, dim3(rb0), dim3(256), 0, stream, w.cls, W, R0, w.row_off,
-                       w.row_soff, w.row_prevw, w.row_prevd, w.lead_dep_pix, w.lead_seg_start,
-                       w.lead_seg_key);
-    (void)hipEventRecord(w.le1, stream);
-    (void)hipStreamWaitEvent(w.lstream, w.le1, 0);
-    hipLaunchKernelGGL(s.n <= kLdsShapes ? k_lead<true> : k_lead<false>, dim3(1),
-                       dim3(kResolveBlock), 0, w.lstream, sc, maxrec, (const DepLine*)w.deprec,
-                       (const long long*)w.lead_dep_pix, (const long long*)w.lead_seg_key,
-                       (const float4*)w.wcarry, (const int*)w.lead_seg_start,
-                       (const int*)w.lead_counters, (CinG*)w.cin, w.epoch, w.coop_group,
-                       w.wave_k, w.long_len / 4, w.lead_pre);
-    (void)hipEventRecord(w.le1, w.lstream);   // re-recorded: now "the leader is done"
-    (void)hipStreamWaitEvent(stream, w.le2, 0);
-    if (ev) (void)hipEventRecord(ev[0], stream);
-    const int row_blocks = (H + kRowWaves - 1) / kRowWaves;
-    const int block_cap = w.resolve_blocks - w.team_blocks - w.helpers - w.headb_first;
-    hipLaunchKernelGGL(k_row_stats, dim3(row_blocks), dim3(256), 0, stream, w.cls, W, H,
-                       (RowStats*)w.row_stats, w.counters, (uint4*)w.team,
-                       (int)(sizeof(TeamState) / sizeof(uint4)), w.batch_state, w.batch_ints);
-    hipLaunchKernelGGL(k_row_scan, dim3(1), dim3(kScanBlock), 0, stream, H,
-                       (const RowStats*)w.row_stats, w.row_off, w.row_soff, w.row_prevw,
-                       w.row_prevd, w.counters);
-    hipLaunchKernelGGL(k_row_compact, dim3(row_blocks), dim3(256), 0, stream, w.cls, W, H,
-                       w.row_off, w.row_soff, w.row_prevw, w.row_prevd, w.dep_pix, w.seg_start,
-                       w.seg_key);
-    hipLaunchKernelGGL(k_seg_order, dim3(1), dim3(kScanBlock), 0, stream, w.seg_start,
-                       w.counters, w.seg_order, w.batch_state, w.batch_cnt, w.batch_rq,
-                       w.block_min, block_cap, w.batch_ints > 0 ? 0 : 1);
-    if (ev) (void)hipEventRecord(ev[1], stream);
-    // the leader stops at its next window; the resolver starts once it has
-    (void)hipMemsetAsync(w.lead_pre + 6, 1, 1, stream);
-    (void)hipStreamWaitEvent(stream, w.le1, 0);
-    auto kr = s.n <= kLdsShapes ? k_resolve<true> : k_resolve<false>;
-    hipLaunchKernelGGL(kr, dim3(w.resolve_blocks), dim3(kResolveBlock), w.resolve_lds, stream,
-                       sc, maxrec, (const DepLine*)w.deprec, w.dep_pix, w.seg_key, w.wcarry,
-                       w.seg_start, w.seg_order, w.counters, w.counters + 1, (CinG*)w.cin,
-                       w.team_blocks, w.long_len, (TeamState*)w.team, w.trace, w.coop_group,
-                       w.wave_k, w.resolve_k, w.resolve_clean > 0 ? w.resolve_clean : 1,
-                       w.team_cscan, w.epoch, w.helpers, w.hand_run, w.inject, w.block_min,
-                       w.headb_first, w.inres ? w.batch_cnt : nullptr, w.batch_rq, cam, W, out,
-                       w.patch, zcount, w.batch_state, w.inres, (const int*)w.lead_pre);
-    if (ev) (void)hipEventRecord(ev[2], stream);
-    enqueue_phase_c(sc, cam, st, W, H, maxrec, out, w, zcount, stream);
-    if (ev) (void)hipEventRecord(ev[3], stream);
-    return hipGetLastError();
-  }
-  // frames in flight with the early leader (rc_tuning.pipe_lead): band 0's phase A and list,
-  // the leader on its lane's CU, then phase A of the other rows; the leader works until the
-  // lane is free for this frame's resolver (the stop flag is set on the lane's stream)
-  const bool plead = w.lead_rows > 0 && w.lead_rows < H && w.rstream && !w.side && w.lstream &&
-                     w.team_blocks > 0;
   if (w.side && w.split_shade)   // carry part only; colours shaded beside the resolver (k_side)
     hipLaunchKernelGGL(st ? k_classify<true> : k_classify<false>, grid, dim3(kBlock), 0, stream, sc, cam, W, H, maxrec, w.cls,
                        w.wcarry, (DepLine*)w.deprec);
-  else if (plead) {
-    const int R0 = w.lead_rows;
-    (void)hipMemsetAsync(w.lead_counters, 0, 16 * sizeof(int), stream);
-    (void)hipMemsetAsync(w.lead_pre, 0, 8 * sizeof(int), stream);
-    dim3 g0((W + kTileW - 1) / kTileW, (R0 + kTileH - 1) / kTileH);
-    hipLaunchKernelGGL(st ? k_phase_a<true> : k_phase_a<false>, g0, dim3(kBlock), 0, stream, sc,
-                       cam, W, 0, 1, R0, maxrec, out, w.cls, w.wcarry, (DepLine*)w.deprec,
-                       zcount, W);
-    const int rb0 = (R0 + kRowWaves - 1) / kRowWaves;
-    hipLaunchKernelGGL(k_row_stats, dim3(rb0), dim3(256), 0, stream, w.cls, W, R0,
-                       (RowStats*)w.row_stats, w.lead_counters, (uint4*)nullptr, 0, (int*)nullptr,
-                       0);
-    hipLaunchKernelGGL(k_row_scan, dim3(1), dim3(kScanBlock), 0, stream, R0,
-                       (const RowStats*)w.row_stats, w.row_off, w.row_soff, w.row_prevw,
-                       w.row_prevd, w.lead_counters);
-    hipLaunchKernelGGL(k_row_compact, dim3(rb0), dim3(256), 0, stream, w.cls, W, R0, w.row_off,
-                       w.row_soff, w.row_prevw, w.row_prevd, w.lead_dep_pix, w.lead_seg_start,
-                       w.lead_seg_key);
-    (void)hipEventRecord(w.le0, stream);
-    (void)hipStreamWaitEvent(w.lstream, w.le0, 0);
-    hipLaunchKernelGGL(s.n <= kLdsShapes ? k_lead<true> : k_lead<false>, dim3(1),
-                       dim3(kResolveBlock), 0, w.lstream, sc, maxrec, (const DepLine*)w.deprec,
-                       (const long long*)w.lead_dep_pix, (const long long*)w.lead_seg_key,
-                       (const float4*)w.wcarry, (const int*)w.lead_seg_start,
-                       (const int*)w.lead_counters, (CinG*)w.cin, w.epoch, w.coop_group,
-                       w.wave_k, w.long_len / 4, w.lead_pre);
-    (void)hipEventRecord(w.le1, w.lstream);
-    const size_t off = (size_t)R0 * W;
-    dim3 g1((W + kTileW - 1) / kTileW, (H - R0 + kTileH - 1) / kTileH);
-    hipLaunchKernelGGL(st ? k_phase_a<true> : k_phase_a<false>, g1, dim3(kBlock), 0, stream,
-                       sc, cam, W, R0, 1, H - R0, maxrec, out + off * 3, w.cls + off,
-                       w.wcarry + off, (DepLine*)w.deprec + off, zcount, W);
-  } else
+  else
     hipLaunchKernelGGL(st ? k_phase_a<true> : k_phase_a<false>, grid, dim3(kBlock), 0, stream, sc, cam, W, 0, 1, H, maxrec, out,
                        w.cls, w.wcarry, (DepLine*)w.deprec, zcount, W);
   if (ev) (void)hipEventRecord(ev[0], stream);
@@ -3242,10 +3047,6 @@ hipError_t launch_parity(const LaunchScene& s, int W, int H, int maxrec, uint8_t
     rs = w.rstream;
     (void)hipEventRecord(w.rready, stream);
     (void)hipStreamWaitEvent(rs, w.rready, 0);
-    if (plead) {   // the lane is free and the list is ready: the leader stops, the team resumes
-      (void)hipMemsetAsync(w.lead_pre + 6, 1, 1, rs);
-      (void)hipStreamWaitEvent(rs, w.le1, 0);
-    }
     if (w.rt0) (void)hipEventRecord(w.rt0, rs);
   }
   hipLaunchKernelGGL(kres, dim3(w.resolve_blocks), dim3(kResolveBlock), w.resolve_lds, rs, sc,
@@ -3254,7 +3055,7 @@ hipError_t launch_parity(const LaunchScene& s, int W, int H, int maxrec, uint8_t
                      w.long_len, (TeamState*)w.team, w.trace, w.coop_group, w.wave_k,
                      w.resolve_k, w.resolve_clean > 0 ? w.resolve_clean : 1, w.team_cscan, w.epoch, w.helpers, w.hand_run, w.inject, w.block_min,
                      w.headb_first, (w.side || w.inres) ? w.batch_cnt : nullptr, w.batch_rq, cam, W, out,
-                     w.patch, zcount, w.batch_state, w.inres, plead ? w.lead_pre : nullptr);
+                     w.patch, zcount, w.batch_state, w.inres);
   if (w.rstream) {
     if (w.rt1) (void)hipEventRecord(w.rt1, rs);
     (void)hipEventRecord(w.rdone, rs);
@@ -3451,7 +3252,7 @@ hipError_t launch_shard_resolve(const LaunchScene& s, int W, int H, int G, int r
                      w.wave_k, w.resolve_k, w.resolve_clean > 0 ? w.resolve_clean : 1,
                      w.team_cscan, w.epoch, w.helpers, w.hand_run, w.inject, w.block_min,
                      w.headb_first, w.inres ? w.batch_cnt : nullptr, w.batch_rq, cam, W, out, (uint32_t*)nullptr,
-                     zcount, w.batch_state, w.inres, (const int*)nullptr);
+                     zcount, w.batch_state, w.inres);
   if (ev) (void)hipEventRecord(ev[1], stream);
   enqueue_phase_c(sc, cam, stage_fits(s), W, H, maxrec, out, w, zcount, stream);
   return hipGetLastError();

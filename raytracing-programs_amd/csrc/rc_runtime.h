@@ -47,9 +47,6 @@ struct FrameBufs {
   DevBuf zcount;        // zero-normalize counter
   DevBuf scene;         // uploaded packed scene
   const void* scene_src = nullptr;   // host image last uploaded
-  // the early leader's band (one frame at a time, ParityWork::lead_rows): counters + leader
-  // record, DEP list, segment keys and starts
-  DevBuf lead, lead_pix, lead_seg;
   DevBuf cls, wcarry, deprec, rows, dep_pix, seg_key, seg_start, seg_order, batch_state, cin,
       counters, team, trace;
 };
@@ -139,11 +136,6 @@ struct Pipe {
   hipStream_t pc[kLanes] = {};
   hipStream_t spare[2] = {};         // pipe_order 3/4: placeholders that keep a queue per lane
   bool pc_shared = false;            // pipe_order 4: both lanes' phase C on one stream (pc[0])
-  // the early leader in frames in flight (rc_tuning.pipe_lead): one CU per lane taken from the
-  // pixel partition, a stream masked to it, and per slot its band's events
-  hipStream_t lstream[kLanes] = {};
-  hipEvent_t lead0[kSlots] = {}, lead1[kSlots] = {};
-  bool lead = false;
   hipEvent_t cdone[kSlots] = {};
   bool cpend[kSlots] = {};           // slot k's phase C is enqueued and not yet synchronised
   hipEvent_t adone[kSlots] = {};     // after slot k's phase A
@@ -198,10 +190,6 @@ struct DevCtx {
   // rc_render's overlapped copy (parity): the framebuffer leaves on `d2h` while the resolver
   // runs, then only the DEP entries' colours (`patch`, packed RGB per entry) follow
   hipStream_t d2h = nullptr;
-  // the early leader (lone parity frames): its one-CU stream, phase A of the other rows on
-  // every other CU, and their events
-  hipStream_t lstream = nullptr, pstream2 = nullptr;
-  hipEvent_t le[3] = {nullptr, nullptr, nullptr};
   DevBuf patch;
   uint8_t* pin_pix = nullptr;     // pinned: DEP pixel indices (int64 per entry)
   uint8_t* pin_patch = nullptr;   // pinned: DEP entries' packed RGB

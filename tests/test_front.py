@@ -221,7 +221,7 @@ def test_tuning_api_validates():
                 dict(team_blocks=-2), dict(resolve_grid=4), dict(split_shade=1, side=0),
                 dict(copy_threads=0), dict(resolve_lds_kb=200), dict(long_len=10), dict(x0=2),
                 dict(pipe_order=5), dict(patch_host=3), dict(share_device=2),
-                dict(headb_first=-1), dict(pipe_last_whole=2), dict(lead_rows=-2), dict(pipe_lead=2)):
+                dict(headb_first=-1), dict(pipe_last_whole=2)):
         with pytest.raises(ValueError):
             rc.set_tuning(**bad)
         assert rc.get_tuning() == base, bad
@@ -230,8 +230,7 @@ def test_tuning_api_validates():
         assert (t["side"], t["helpers"], t["team_blocks"]) == (0, 1, 24)
     assert rc.get_tuning() == base
     # the round-5 fields round-trip, and their defaults are the measured schedule
-    assert (base["share_device"], base["headb_first"], base["pipe_last_whole"],
-            base["lead_rows"]) == (0, 24, 1, -1)
+    assert (base["share_device"], base["headb_first"], base["pipe_last_whole"]) == (0, 24, 1)
     with rc.tuned(headb_first=0, share_device=1, pipe_last_whole=0):
         t = rc.get_tuning()
         assert (t["headb_first"], t["share_device"], t["pipe_last_whole"]) == (0, 1, 0)

@@ -75,8 +75,7 @@ SCHEDULES = {"no-side": dict(side=0), "side-always": dict(side=1), "side-by-size
              "device-patch": dict(patch_host=0),
              "mapped-patch-after-frame": dict(patch_host=1),
              "helpers-8-hand-run-512": dict(helpers=8, hand_run=512),
-             "no-headb-first": dict(headb_first=0), "no-early-leader": dict(lead_rows=0),
-             "early-leader-1-row": dict(lead_rows=1)}
+             "no-headb-first": dict(headb_first=0)}
 
 
 @pytest.mark.parametrize("sched", list(SCHEDULES))
@@ -299,8 +298,6 @@ PIPES = {"default": {},
          "stream-order-1": dict(pipe_order=1),
          "queue-per-lane": dict(pipe_order=3),
          "one-phase-c-stream": dict(pipe_order=4),
-         "early-leader": dict(pipe_lead=1),
-         "early-leader-slot-streams": dict(pipe_lead=1, pipe_slotstreams=1),
          "last-phase-c-on-partition": dict(pipe_last_whole=0)}
 
 
@@ -809,30 +806,4 @@ def test_held_back_phase_c_completion_points(scenes, table):
     rc.frame_submit(s, n, n, bufs[1].data_ptr(), depth=6)
     rc.frames_wait(tim)
     assert (tim["frames_checked"], tim["frames_failed"]) == (1, 0)
-    assert rc.lone_frames_check()["failed"] == 0
-
-
-@pytest.mark.parametrize("lead", [0, 1, 3, 64, 128, 161, 204, 370, 1000, -1])
-def test_early_leader_bands(lead, scenes, table):
-    """The early leader (rc_tuning.lead_rows, k_lead): phase A and the DEP list of the first
-    `lead` rows, then one workgroup on a CU of its own resolves the band's last segment while
-    phase A of the other rows runs, and the resolver's team resumes that segment.  The band is
-    only a schedule: every image equals the reference's, for bands that end inside, before or
-    after the team segment (simple 1024^2 d6: its 88k-entry segment spans rows 161-369; quadric
-    4096^2: rows 0-816), bands of one row, and the default (-1 = H/32); lone frames through the
-    drop-in path and device-resident, every hand-off verified."""
-    torch = pytest.importorskip("torch")
-    keys = ["simple:1024x1024:d6:parity", "quadric:4096x4096:d6:parity",
-            "reflection:2048x2048:d4:parity", "quadric:333x517:d6:parity"]
-    rc.lone_frames_check()
-    with rc.tuned(lead_rows=lead):
-        for key in keys:
-            scene, size, d, mode = key.split(":")
-            w, h = map(int, size.split("x"))
-            assert p3_md5(rc.render(scenes[scene], w, h, depth=int(d[1:]), mode=mode)) == \
-                table[key]["md5"], (lead, key)
-            out = torch.empty((h, w, 3), dtype=torch.uint8, device="cuda")
-            rc.render_device(scenes[scene], w, h, out.data_ptr(), depth=int(d[1:]), mode=mode)
-            torch.cuda.synchronize()
-            assert p3_md5(out.cpu().numpy()) == table[key]["md5"], ("device", lead, key)
     assert rc.lone_frames_check()["failed"] == 0
