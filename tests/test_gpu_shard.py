@@ -231,12 +231,23 @@ def test_render_num_gpus_shared_device(G, mode, scenes, table):
                 assert t["dep_pixels"] == 2804464
 
 
-def test_render_num_gpus_clamped_warns(scenes, table, capfd):
+def test_render_num_gpus_clamped_warns(table):
     """More GPUs than the box has (one here, unless the box is bigger): rc_render renders on
-    the devices there are and says so on stderr (once per process), md5 unchanged."""
-    ndev = torch.cuda.device_count()
-    key = "quadric:256x256:d6:parity"
-    img = rc.render(scenes["quadric"], 256, 256, depth=6, gpus=ndev + 3)
-    assert p3_md5(img) == table[key]["md5"]
-    err = capfd.readouterr().err
-    assert f"{ndev + 3} GPUs requested" in err and f"rendering on {ndev}" in err
+    the devices there are and says so on stderr, md5 unchanged.  The warning is printed once
+    per process, so the check runs in a fresh process (an earlier clamp in the test
+    process would otherwise have used it up)."""
+    import subprocess
+    import sys
+    tests = os.path.dirname(os.path.abspath(__file__))
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "import torch\n"
+            "from helpers import p3_md5, rc, scene_path\n"
+            "n = torch.cuda.device_count()\n"
+            "s = rc.Scene.from_file(scene_path('quadric'))\n"
+            "img = rc.render(s, 256, 256, depth=6, gpus=n + 3)\n"
+            "print('RESULT', p3_md5(img), n, flush=True)\n" % tests)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    _, md5, n = [l for l in r.stdout.splitlines() if l.startswith("RESULT")][-1].split()
+    assert md5 == table["quadric:256x256:d6:parity"]["md5"]
+    assert f"{int(n) + 3} GPUs requested" in r.stderr and f"rendering on {n}" in r.stderr, r.stderr
