@@ -121,6 +121,10 @@ def test_run_ranks_relays_codes_and_kills_stuck_ranks():
 def test_self_launch_end_to_end_without_gpu():
     """`bench.py --gpus 2` with no launcher starts two ranks; here (no GPU) each rank stops
     with its own message before any GPU call and the parent exits with their status."""
+    import torch
+    if torch.cuda.device_count() > 0:   # counting devices does not initialise HIP
+        import pytest
+        pytest.skip("needs a box without GPUs (the ranks would start rendering)")
     env = {k: v for k, v in os.environ.items()
            if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "RC_BENCH_BACKEND")}
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
