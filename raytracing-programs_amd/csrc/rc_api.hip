@@ -380,18 +380,21 @@ int ensure_pinned(DevCtx& c, size_t entries) {
 
 // patch_host: the DEP entries' packed colours go straight to pinned, mapped host memory from
 // phase C's stores (a batch of 64 entries is one 256-byte write), during the resolver, instead
-// of an 11 MB copy (quadric 4096^2) after the frame's last kernel.  Entries carry a ready mark
-// (kPatchReady), so for patch_host 2 the array must start the frame cleared: that scatter clears
-// what it consumes; patch_host 1's (and a frame that ended early) leave host_patch_dirty entries.
-// rc_render raises host_patch_dirty to the whole image before it enqueues a frame that writes
-// the array and lowers it to the frame's DEP count once that is known, so a frame that fails
-// before then still has its marks cleared.
-int ensure_host_patch(DevCtx& c, size_t entries, int patch_host) {
+// of an 11 MB copy (quadric 4096^2) after the frame's last kernel.  Each entry carries its
+// frame's mark (rc::patch_mark of the frame's epoch) and the host never stores to the array
+// while a frame runs: a frame's entries are known by the mark alone.  Marks repeat every
+// rc::kPatchMarks epochs, so before a frame of epoch `epoch` is enqueued the array's possibly
+// marked entries (host_patch_dirty) are cleared once `epoch` is that far past the last clear.  rc_render
+// raises host_patch_dirty to the whole image before it enqueues a frame that writes the array
+// and lowers it to the largest DEP count since the clear once the frame's own is known.
+int ensure_host_patch(DevCtx& c, size_t entries, unsigned epoch) {
   if (entries <= c.host_patch_entries) {
-    if (patch_host == 2 && c.host_patch_dirty) {
+    if (c.host_patch_dirty &&
+        (epoch <= c.host_patch_epoch0 || epoch - c.host_patch_epoch0 >= rc::kPatchMarks)) {
       std::memset(c.host_patch, 0, c.host_patch_dirty * sizeof(uint32_t));
       c.host_patch_dirty = 0;
     }
+    if (!c.host_patch_dirty) c.host_patch_epoch0 = epoch - 1;   // nothing marked
     return 0;
   }
   if (c.host_patch) (void)hipHostFree(c.host_patch);
@@ -405,57 +408,82 @@ int ensure_host_patch(DevCtx& c, size_t entries, int patch_host) {
   c.host_patch_entries = entries;
   std::memset(c.host_patch, 0, entries * sizeof(uint32_t));
   c.host_patch_dirty = 0;
+  c.host_patch_epoch0 = epoch - 1;
   return 0;
 }
 
 // The scatter of a mapped colour patch while the frame still runs (patch_host): each host
-// thread sweeps its share of the DEP list, scatters every entry phase C has marked ready and
-// clears it, until its share is done; once the frame's last kernel has completed (ev_done),
-// one more sweep takes everything left.  The framebuffer copy must already be in `host` (it
-// carries the DEP pixels' phase-A bytes, which the patch overwrites).  A sweep that found
-// nothing yields before the next; any event status other than "not ready" ends every thread's
-// sweeps (the frame failed: returns -1, the caller reports it).
-int scatter_progressive(DevCtx& c, uint8_t* host, const long long* pix, uint32_t* patch,
-                        size_t ndep, hipEvent_t ev_done) {
+// thread sweeps its share of the DEP list and scatters every entry phase C has marked, until
+// its share is done; once the frame's last kernel has completed (ev_done), one more sweep takes
+// everything left.  The framebuffer copy must already be in `host` (it carries the DEP pixels'
+// phase-A bytes, which the patch overwrites).  The array is only read: an entry is this
+// frame's once its top byte is `mark`.
+// A thread's share is a contiguous run of blocks of kScatterBlock entries (phase C's batch, one
+// 256-byte store; contiguous, so its pixels are a band of rows: spreading every thread over the
+// whole image made the scatter itself ~5x slower per entry, TLB and cache misses on the
+// caller's pixmap, profiles/r06n_scatter_diag.txt); a block stays on the thread's pending list
+// with a cursor at its first unconsumed entry, and a sweep before the frame's end moves on to
+// the next block at the first entry not yet marked, so a sweep costs about one read per
+// pending block rather than one per entry left.  A sweep that found nothing yields; the event is
+// queried by one thread at a time, at most once per kScatterQueryNs (every thread querying
+// after each short sweep contends in the runtime); any status other than "not ready" ends
+// every thread's sweeps (the frame failed: returns -1, the caller reports it).
+constexpr size_t kScatterBlock = 64;
+constexpr long long kScatterQueryNs = 20000;
+
+int scatter_progressive(DevCtx& c, uint8_t* host, const long long* pix, const uint32_t* patch,
+                        size_t ndep, uint32_t mark, hipEvent_t ev_done) {
   std::atomic<bool> over{false};
   std::atomic<int> status{(int)hipSuccess};
+  std::atomic<long long> next_query{0};
+  const auto t0 = std::chrono::steady_clock::now();
+  const size_t nblk = (ndep + kScatterBlock - 1) / kScatterBlock;
   HostPool::get(c.device).run([&](int part, int parts) {
-    const size_t per = (ndep + parts - 1) / parts;
-    const size_t a = (size_t)part * per, b = a + per < ndep ? a + per : ndep;
-    if (a >= b) return;
-    size_t left = b - a, lo = a;   // lo: entries below it are all consumed
+    std::vector<size_t> pend;   // per pending block: its first unconsumed entry
+    pend.reserve(nblk / parts + 1);
+    const size_t per = (nblk + parts - 1) / parts;
+    for (size_t k = (size_t)part * per; k < nblk && k < (size_t)(part + 1) * per; ++k)
+      pend.push_back(k * kScatterBlock);
+    if (pend.empty()) return;
     for (;;) {
       const bool last = over.load(std::memory_order_acquire);
       if (status.load(std::memory_order_relaxed) != (int)hipSuccess) return;
-      size_t got = 0;
-      bool gap = false;
-      for (size_t j = lo; j < b; ++j) {
-        volatile uint32_t* e = patch + j;
-        const uint32_t v = *e;
-        if (!(v & rc::kPatchReady)) {
-          gap = true;
-          continue;
+      size_t got = 0, keep = 0;
+      for (size_t i = 0; i < pend.size(); ++i) {
+        size_t j = pend[i];
+        const size_t end = std::min((j / kScatterBlock + 1) * kScatterBlock, ndep);
+        for (; j < end; ++j) {
+          const uint32_t v = *(const volatile uint32_t*)(patch + j);
+          if ((v & 0xFF000000u) != mark) {
+            if (last) continue;   // after the frame an unmarked entry stays unmarked
+            break;
+          }
+          uint8_t* q = host + 3 * (size_t)pix[j];
+          q[0] = (uint8_t)v;
+          q[1] = (uint8_t)(v >> 8);
+          q[2] = (uint8_t)(v >> 16);
+          ++got;
         }
-        uint8_t* q = host + 3 * (size_t)pix[j];
-        q[0] = (uint8_t)v;
-        q[1] = (uint8_t)(v >> 8);
-        q[2] = (uint8_t)(v >> 16);
-        *e = 0;
-        ++got;
-        if (!gap) lo = j + 1;
+        if (j < end) pend[keep++] = j;
       }
-      left -= got;
-      if (!left || last) return;   // after the frame an unmarked entry stays unmarked
-      if (!got) {
-        const hipError_t q = hipEventQuery(ev_done);
-        if (q == hipSuccess) {
-          over.store(true, std::memory_order_release);
-        } else if (q != hipErrorNotReady) {
-          status.store((int)q, std::memory_order_relaxed);
-          return;
-        } else {
-          std::this_thread::yield();
-        }
+      pend.resize(keep);
+      if (pend.empty() || last) return;
+      if (got) continue;
+      const long long now = std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                std::chrono::steady_clock::now() - t0).count();
+      long long due = next_query.load(std::memory_order_relaxed);
+      if (now < due || !next_query.compare_exchange_strong(due, now + kScatterQueryNs)) {
+        std::this_thread::yield();
+        continue;
+      }
+      const hipError_t q = hipEventQuery(ev_done);
+      if (q == hipSuccess) {
+        over.store(true, std::memory_order_release);
+      } else if (q != hipErrorNotReady) {
+        status.store((int)q, std::memory_order_relaxed);
+        return;
+      } else {
+        std::this_thread::yield();
       }
     }
   });
@@ -503,9 +531,10 @@ thread_local E2eTrace* g_e2e = nullptr;
 // pixels), and the host pool scatters them over the copy — or, with patch_host, phase C wrote
 // them into mapped host memory and the pool scatters each as it arrives (scatter_progressive),
 // so only the frame's last entries are left once it ends.
-// host_patch: the mapped array phase C writes (patch_host 1 or 2, tu.patch_host says which);
-// prev_dirty: its entries an earlier frame may have left marked (rc_render has raised
-// host_patch_dirty to the whole image for this frame; it drops to the frame's own bound here).
+// host_patch: the mapped array phase C writes (patch_host 1 or 2, tu.patch_host says which),
+// its entries marked with rc::patch_mark of this frame's epoch (c.fb.epoch); prev_dirty: its
+// entries marked since the last clear before this frame (rc_render has raised host_patch_dirty
+// to the whole image for this frame; it drops to the bound of both here).
 int copy_overlapped(DevCtx& c, uint8_t* host, const uint8_t* dev, size_t bytes,
                     const hipEvent_t* ev, uint32_t* host_patch, size_t prev_dirty,
                     const rc_tuning& tu) {
@@ -518,6 +547,7 @@ int copy_overlapped(DevCtx& c, uint8_t* host, const uint8_t* dev, size_t bytes,
   const size_t ndep = (size_t)c.pin_cnt[2];
   // the frame writes (and marks) only entries below its DEP count
   if (host_patch) c.host_patch_dirty = std::max(prev_dirty, ndep);
+  const uint32_t mark = rc::patch_mark(c.fb.epoch);
   if (ensure_pinned(c, ndep)) return -1;
   if (ndep)
     HIP_TRY(hipMemcpyAsync(c.pin_pix, c.fb.dep_pix.p, ndep * sizeof(long long),
@@ -526,12 +556,10 @@ int copy_overlapped(DevCtx& c, uint8_t* host, const uint8_t* dev, size_t bytes,
   if (g_e2e) g_e2e->mark(3);
   if (host_patch && ndep && tu.patch_host == 2) {   // consumed as it arrives
     HIP_TRY(hipStreamSynchronize(c.d2h));   // the DEP list's copy
-    if (scatter_progressive(c, host, (const long long*)c.pin_pix, host_patch, ndep, ev[4]))
+    if (scatter_progressive(c, host, (const long long*)c.pin_pix, host_patch, ndep, mark,
+                            ev[4]))
       return -1;
     HIP_TRY(hipEventSynchronize(ev[4]));
-    // every entry below ndep consumed and cleared, none written above it; entries an earlier
-    // frame left marked were cleared before this frame (ensure_host_patch)
-    c.host_patch_dirty = 0;
     if (g_e2e) {
       g_e2e->mark(4);
       g_e2e->mark(5);
@@ -716,6 +744,11 @@ int upload_scene(FrameBufs& b, hipStream_t stream, const rc_scene* s, rc::Launch
   return 0;
 }
 
+// The epoch of a workspace's next parity frame: tags keep bit 31 for a flag, so they wrap to 1
+// (ensure_parity then clears the carry-ins once; a fresh buffer starts at tag 0, which no frame
+// uses).
+unsigned next_epoch(unsigned e) { return e + 1 >= 0x80000000u ? 1u : e + 1; }
+
 // res_cus: CUs the resolver grid may occupy (all of them, or the pipeline's partition);
 // piped: a pipeline lane (< 0: whenever res_cus is not the whole device).
 int ensure_parity(DevCtx& c, FrameBufs& b, int W, int H, rc::ParityWork& w, int res_cus,
@@ -738,10 +771,8 @@ int ensure_parity(DevCtx& c, FrameBufs& b, int W, int H, rc::ParityWork& w, int 
     if (b.cin.ensure(P * rc::kCinBytes) || hipMemset(b.cin.p, 0, P * rc::kCinBytes) != hipSuccess)
       return -1;
   }
-  if (++b.epoch >= 0x80000000u) {   // wrapped (tags keep bit 31 for a flag): clear once
-    if (hipMemset(b.cin.p, 0, b.cin.bytes) != hipSuccess) return -1;
-    b.epoch = 1;
-  }
+  b.epoch = next_epoch(b.epoch);
+  if (b.epoch == 1 && hipMemset(b.cin.p, 0, b.cin.bytes) != hipSuccess) return -1;
   const bool piped = piped_lane >= 0 ? piped_lane != 0 : res_cus != c.cus;
   // Resolver placement by its dynamic LDS reservation: one workgroup (4 waves, one per SIMD)
   // per CU for a lone frame, whose critical path is its carry chains (and k_side must stay off
@@ -1748,10 +1779,11 @@ int rc_render(const rc_scene* s, int W, int H, const rc_options* opt, uint8_t* p
   uint32_t* patch = nullptr;
   const bool hpatch = overlap && tu.patch_host;
   size_t prev_dirty = 0;
+  const unsigned epoch = next_epoch(c->fb.epoch);   // the frame's (ensure_parity assigns it)
   if (overlap) {
     if (!c->d2h && hipStreamCreateWithFlags(&c->d2h, hipStreamNonBlocking) != hipSuccess) return -1;
     if (hpatch) {
-      if (ensure_host_patch(*c, (size_t)W * H, tu.patch_host)) return -1;
+      if (ensure_host_patch(*c, (size_t)W * H, epoch)) return -1;
       patch = c->host_patch_dev;
       // until the frame's DEP count is known (copy_overlapped), any entry may get a mark
       prev_dirty = c->host_patch_dirty;
@@ -1770,6 +1802,10 @@ int rc_render(const rc_scene* s, int W, int H, const rc_options* opt, uint8_t* p
   } unset;
   if (E2eTrace::on()) g_e2e = &trace;
   if (enqueue_render(*c, s, W, H, 0, 1, H, opt, d_out, c->stream, true, patch, &ev)) return -1;
+  if (hpatch && c->fb.epoch != epoch) {   // the array's clearing assumed this epoch
+    std::fprintf(stderr, "Error: rc_render: frame epoch %u, expected %u\n", c->fb.epoch, epoch);
+    return -1;
+  }
   // the frame's counts for rc_timing / raycast()'s stderr lines, behind its last kernel
   if (!c->pin_tail) HIP_TRY(hipHostMalloc((void**)&c->pin_tail, 64, hipHostMallocDefault));
   HIP_TRY(hipMemcpyAsync(c->pin_tail, c->fb.zcount.p, 8, hipMemcpyDeviceToHost, c->stream));

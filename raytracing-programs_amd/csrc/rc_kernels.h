@@ -83,8 +83,8 @@ struct ParityWork {
 
 constexpr int kSegOrderMax = 65536;   // segments ordered for the resolver queue (else FIFO)
 constexpr int kCinBytes = 24;         // one carry-in = three tagged 8-byte granules
-constexpr int kLdsShapesMax = 64;
-constexpr int kDenseSlots = 64;       // k_resolve's hand-off ring (helper workgroups at most)     // k_resolve stages up to this many shapes in LDS
+constexpr int kLdsShapesMax = 64;     // k_resolve stages up to this many shapes in LDS
+constexpr int kDenseSlots = 64;       // k_resolve's hand-off ring (helper workgroups at most)
 
 // cuda_sem: RC_MODE_CUDA (the CUDA port's arithmetic, rc_cudasem.hpp) instead of fast mode
 hipError_t launch_render(const LaunchScene& s, int W, int H, int row0, int row_step, int nrows,
@@ -95,9 +95,19 @@ hipError_t launch_parity(const LaunchScene& s, int W, int H, int maxrec, uint8_t
                          const ParityWork& w, unsigned long long* zcount, hipStream_t stream,
                          const hipEvent_t* ev);
 
-// Top byte of a colour-patch entry (ParityWork::patch) once phase C has stored it; the low three
-// bytes are R, G, B.  rc_render's host side consumes marked entries and clears them to 0.
-constexpr uint32_t kPatchReady = 0xFF000000u;
+// Top byte of a colour-patch entry (ParityWork::patch) once phase C has stored it: the frame's
+// mark, 0x80 | (epoch & 0x7f) of its carry-in epoch (never 0, the cleared value); the low three
+// bytes are R, G, B.  rc_render's host side
+// only reads the array during a frame (an entry is this frame's once its top byte is this
+// frame's mark) and never stores to it then: a host store into a line that phase C is still
+// writing in pieces (k_dep_chunks) was seen undone by the device's later store to that line,
+// leaving a stale mark (round 6, profiles/r06n_patch_marks.txt).  Marks of kPatchMarks
+// consecutive epochs are distinct, so the array is cleared once per kPatchMarks epochs
+// (ensure_host_patch).
+constexpr unsigned kPatchMarks = 128;
+__host__ __device__ constexpr uint32_t patch_mark(unsigned epoch) {
+  return (epoch << 24) | 0x80000000u;
+}
 
 // Phase C of a frame launched with defer_c: waits for w.rdone on `stream`.
 hipError_t launch_phase_c(const LaunchScene& s, int W, int H, int maxrec, uint8_t* out,

@@ -178,17 +178,17 @@ __device__ __forceinline__ void store_rgb(uint8_t* __restrict__ p, V3 c) {
 
 // Phase C's store of DEP entry j at pixel p: the framebuffer, and — when the host is copying
 // the framebuffer out while the resolver runs (rc_render) — the entry's packed RGB in `patch`,
-// which the host then scatters over the DEP pixels of its copy.  The top byte is a ready mark
-// (kPatchReady): one 4-byte store carries colour and mark together, so a host reading mapped
-// memory during the frame scatters an entry as soon as it sees the mark, and clears it.
+// which the host then scatters over the DEP pixels of its copy.  The top byte is the frame's
+// mark (patch_mark of its epoch `tag`): one 4-byte store carries colour and mark together, so a
+// host reading mapped memory during the frame scatters an entry as soon as it sees the mark.
 __device__ __forceinline__ void store_dep(uint8_t* __restrict__ out, uint32_t* __restrict__ patch,
-                                          long long p, int j, V3 c) {
+                                          unsigned tag, long long p, int j, V3 c) {
   const uint8_t r = quant(c.x), g = quant(c.y), b = quant(c.z);
   uint8_t* q = out + (size_t)p * 3;
   q[0] = r;
   q[1] = g;
   q[2] = b;
-  if (patch) patch[j] = kPatchReady | (uint32_t)r | ((uint32_t)g << 8) | ((uint32_t)b << 16);
+  if (patch) patch[j] = patch_mark(tag) | (uint32_t)r | ((uint32_t)g << 8) | ((uint32_t)b << 16);
 }
 
 __device__ __forceinline__ void flush_events(int zero_events, unsigned long long* counter) {
@@ -1709,7 +1709,8 @@ __device__ __forceinline__ void shade_batch(const Scene& sc, const Cam& cam, int
                                             const long long* __restrict__ dep_pix,
                                             const DepLine* __restrict__ deprec, int ndep, int b,
                                             V3 c, bool hit, uint8_t* __restrict__ out,
-                                            uint32_t* __restrict__ patch, int& zero) {
+                                            uint32_t* __restrict__ patch, unsigned tag,
+                                            int& zero) {
   const int j = b * 64 + (int)(threadIdx.x & 63);
   if (j >= ndep) return;
   const long long p = dep_pix[j];
@@ -1720,14 +1721,14 @@ __device__ __forceinline__ void shade_batch(const Scene& sc, const Cam& cam, int
     } else {
       rgb = dep_pcol(deprec + p);
     }
-    store_dep(out, patch, p, j, rgb);
+    store_dep(out, patch, tag, p, j, rgb);
     return;
   }
   const int y = (int)(p / W), x = (int)(p % W);
   const V3 d = primary_dir(cam, x, y, zero);
   PixelOut po;
   shoot<kModeParityC>(sc, d, maxrec, c, po, zero);
-  store_dep(out, patch, p, j, po.rgb);
+  store_dep(out, patch, tag, p, j, po.rgb);
 }
 
 __device__ __forceinline__ int wave_ticket(int* ctr) {
@@ -1782,7 +1783,7 @@ __device__ __forceinline__ void phase_c_passes(const Scene& sc, const Cam& cam, 
     int mine = 0;
     if ((threadIdx.x & 63) == 0) mine = batch_claim(batch_state, b);
     if (!__shfl(mine, 0, 64)) continue;
-    shade_batch(sc, cam, W, maxrec, dep_pix, deprec, ndep, b, c, hit, out, patch, zero);
+    shade_batch(sc, cam, W, maxrec, dep_pix, deprec, ndep, b, c, hit, out, patch, tag, zero);
     if ((threadIdx.x & 63) == 0) atomicAdd(done_ctr, 1);
   }
   for (;;) {
@@ -1794,7 +1795,7 @@ __device__ __forceinline__ void phase_c_passes(const Scene& sc, const Cam& cam, 
     V3 c = v3(0.0f, 0.0f, 0.0f);
     bool hit = true;
     (void)batch_carries(cin, ndep, b, tag, true, c, hit, ts);
-    shade_batch(sc, cam, W, maxrec, dep_pix, deprec, ndep, b, c, hit, out, patch, zero);
+    shade_batch(sc, cam, W, maxrec, dep_pix, deprec, ndep, b, c, hit, out, patch, tag, zero);
     if ((threadIdx.x & 63) == 0) atomicAdd(done_ctr, 1);
   }
 }
@@ -1864,7 +1865,7 @@ __device__ __forceinline__ void phase_c_ready(const Scene& sc, const Cam& cam, i
     bool hit = true;
     if (tq && (threadIdx.x & 63) == 0) tq[3 * k + 1] = (unsigned)__builtin_amdgcn_s_memrealtime();
     (void)batch_carries(cin, ndep, b, tag, true, c, hit, ts);   // published: arrives at once
-    shade_batch(sc, cam, W, maxrec, dep_pix, deprec, ndep, b, c, hit, out, patch, zero);
+    shade_batch(sc, cam, W, maxrec, dep_pix, deprec, ndep, b, c, hit, out, patch, tag, zero);
     if ((threadIdx.x & 63) == 0) atomicAdd(&counters[9], 1);
     if (tq && (threadIdx.x & 63) == 0) tq[3 * k + 2] = (unsigned)__builtin_amdgcn_s_memrealtime();
   }
@@ -2705,7 +2706,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_
       const bool hv = in && (!kFast || hit);
       if (in && !hv) {
         const long long p = dep_pix[j];
-        store_dep(out, patch, p, j, dep_pcol(deprec + p));
+        store_dep(out, patch, tag, p, j, dep_pcol(deprec + p));
       }
       const unsigned long long m = __ballot(hv);
       int base = 0;
@@ -2735,7 +2736,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RC_
         shoot<kModeParityC>(sc, d, maxrec, c, po, zero);
         rgb = po.rgb;
       }
-      store_dep(out, patch, p, j, rgb);
+      store_dep(out, patch, tag, p, j, rgb);
     }
     __syncthreads();   // the list is rebuilt for the next chunk
   }

@@ -199,7 +199,8 @@ struct DevCtx {
   uint32_t* host_patch = nullptr;     // pinned, mapped: phase C's packed RGB per DEP entry
   uint32_t* host_patch_dev = nullptr; // its device address (patch_host)
   size_t host_patch_entries = 0;
-  size_t host_patch_dirty = 0;       // entries below it may hold an earlier frame's ready mark
+  size_t host_patch_dirty = 0;       // entries below it may hold a mark since the last clear
+  unsigned host_patch_epoch0 = 0;    // epoch before the first frame since that clear
   FrameLog lone_log;   // every parity frame rendered in `fb` (rc_render, rc_render_device)
   // rc_resolver_stats: the last rc_frames_wait window's record (frames in flight), and the
   // resolver placement of the last frame of each kind (grid, CUs it may use)
@@ -228,7 +229,7 @@ int fill_resolver_stats(DevCtx& c, const FrameLog::Diag& d, int grid, int res_cu
 // the host-side copy helpers take the caller's one tuning snapshot (rc_render)
 int copy_to_host(DevCtx& c, uint8_t* host, const uint8_t* dev, size_t bytes, hipStream_t st,
                  const rc_tuning& tu);
-int ensure_host_patch(DevCtx& c, size_t entries, int patch_host);
+int ensure_host_patch(DevCtx& c, size_t entries, unsigned epoch);
 void prefault(DevCtx& c, uint8_t* p, size_t n, const rc_tuning& tu);
 int upload_scene(FrameBufs& b, hipStream_t stream, const rc_scene* s, rc::LaunchScene& ls);
 int ensure_parity(DevCtx& c, FrameBufs& b, int W, int H, rc::ParityWork& w, int res_cus,

@@ -776,6 +776,25 @@ def test_resolver_diagnostics_record(scenes, table):
     assert p3_md5(out.cpu().numpy()) == want
 
 
+@pytest.mark.parametrize("sched", ["default", "no-side"])
+def test_mapped_patch_marks_across_frames(sched, scenes, table):
+    """rc_render's mapped colour patch (patch_host 2) over a run of frames of different scenes
+    and sizes, past two cycles of its per-frame marks (rc::kPatchMarks = 128 epochs, then the
+    array is cleared): every frame's bytes are its golden's.  A mark that outlives its frame
+    makes the next frame scatter an earlier scene's colour (profiles/r06n_patch_marks.txt: seen
+    with phase C after the resolver, side=0, when the host cleared consumed entries)."""
+    keys = ["reflection:256x256:d6:parity", "quadric:256x256:d6:parity",
+            "simple:256x256:d4:parity", "quadric:333x517:d6:parity"]
+    tune = {} if sched == "default" else dict(side=0)
+    with rc.tuned(**tune):
+        for i in range(300):
+            key = keys[i % len(keys)]
+            scene, size, d, mode = key.split(":")
+            w, h = map(int, size.split("x"))
+            img = rc.render(scenes[scene], w, h, depth=int(d[1:]), mode=mode)
+            assert p3_md5(img) == table[key]["md5"], (sched, i, key)
+
+
 def test_held_back_phase_c_completion_points(scenes, table):
     """the last submitted frame's phase C is held back until the next submit or
     rc_frames_wait.  rc_lone_frames_check and a lone render launch it first, so a device
