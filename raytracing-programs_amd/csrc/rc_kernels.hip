@@ -1473,8 +1473,16 @@ __device__ __forceinline__ int block_window(const Scene& sc, int maxrec, BlockWi
 // each block publishes {first changer position, carry x, y, z} as four granules
 // {payload:32, round:32} with agent-scope (sc1) stores; a reader spins on the granules
 // themselves until every tag equals the round, so no counter, fence or drain sits on the
-// path.  Slots are double-buffered by round parity (a block writes round r+1 only after it
-// has read every round-r slot, and nobody reaches round r+2 before everyone read round r+1).
+// path.  Slots rotate over kTeamBufs rounds.  A SCAN round is all-to-all (every block
+// publishes, every block collects every slot), a RESOLVE round is one-to-all (block 0
+// publishes, every block collects it), and RESOLVE rounds never follow each other.  So while
+// a slow block still reads round r, the others can publish at most up to round r + 2: after
+// a SCAN round r, a RESOLVE round r + 1 waits for nobody but block 0, and the SCAN round r + 2
+// cannot be collected without the slow block's own publish.  Round parity (two buffers) let
+// round r + 2 overwrite a round-r slot still unread: the reader then spun out its 5 s limit
+// on a tag it would never see (1 frame in ~200-300 with split shading, whose k_side work slows
+// the team's collects; profiles/r06o_team_slot_race.txt).
+constexpr int kTeamBufs = 4;
 struct alignas(32) TeamSlot {
   unsigned long long g[4];
 };
@@ -1524,7 +1532,7 @@ struct TeamState {
   // missed it)
   int team_row;
   int pad[16];
-  TeamSlot slot[2][kTeamMax];
+  TeamSlot slot[kTeamBufs][kTeamMax];
   DenseQueue dq;
 };
 
@@ -1604,7 +1612,7 @@ __device__ __forceinline__ void ready_range(int* __restrict__ cnt, int* __restri
 }
 
 __device__ __forceinline__ void team_publish(TeamState* ts, int round, unsigned pos, V3 c) {
-  TeamSlot* sl = &ts->slot[round & 1][blockIdx.x];
+  TeamSlot* sl = &ts->slot[round & (kTeamBufs - 1)][blockIdx.x];
   const unsigned tag = (unsigned)round;
   __hip_atomic_store(&sl->g[0], pack2(pos, tag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __hip_atomic_store(&sl->g[1], pack2(__float_as_uint(c.x), tag), __ATOMIC_RELAXED,
@@ -1618,7 +1626,7 @@ __device__ __forceinline__ void team_publish(TeamState* ts, int round, unsigned 
 // Spin until block b's round-`round` slot is complete; returns false on timeout.
 __device__ __forceinline__ bool team_collect(TeamState* ts, int round, int b, unsigned& pos,
                                              V3& c) {
-  TeamSlot* sl = &ts->slot[round & 1][b];
+  TeamSlot* sl = &ts->slot[round & (kTeamBufs - 1)][b];
   const unsigned tag = (unsigned)round;
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   for (;;) {
