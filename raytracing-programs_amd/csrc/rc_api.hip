@@ -17,6 +17,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -418,17 +419,19 @@ int ensure_host_patch(DevCtx& c, size_t entries, unsigned epoch) {
 // everything left.  The framebuffer copy must already be in `host` (it carries the DEP pixels'
 // phase-A bytes, which the patch overwrites).  The array is only read: an entry is this
 // frame's once its top byte is `mark`.
-// A thread's share is a contiguous run of blocks of kScatterBlock entries (phase C's batch, one
-// 256-byte store; contiguous, so its pixels are a band of rows: spreading every thread over the
-// whole image made the scatter itself ~5x slower per entry, TLB and cache misses on the
-// caller's pixmap, profiles/r06n_scatter_diag.txt); a block stays on the thread's pending list
-// with a cursor at its first unconsumed entry, and a sweep before the frame's end moves on to
-// the next block at the first entry not yet marked, so a sweep costs about one read per
-// pending block rather than one per entry left.  A sweep that found nothing yields; the event is
+// Entries go in blocks of kScatterBlock (phase C's batch, one 256-byte store), each with a
+// cursor at its first unconsumed entry; a sweep before the frame's end moves on to the next
+// block at the first entry not yet marked, so it costs about one read per pending block rather
+// than one per entry left.  Blocks go in chunks a thread locks while it sweeps them.  A thread
+// sweeps its own band of chunks (contiguous, so its pixels are a band of rows: spreading every
+// thread over the whole image made the scatter ~5x slower per entry, TLB and cache misses on
+// the caller's pixmap, profiles/r06n_scatter_diag.txt) and, once its band is done, helps with
+// the others'.  A sweep that found nothing yields; the event is
 // queried by one thread at a time, at most once per kScatterQueryNs (every thread querying
 // after each short sweep contends in the runtime); any status other than "not ready" ends
 // every thread's sweeps (the frame failed: returns -1, the caller reports it).
 constexpr size_t kScatterBlock = 64;
+constexpr size_t kScatterChunk = 32;   // blocks per chunk: the unit a thread locks (2048 entries)
 constexpr long long kScatterQueryNs = 20000;
 
 int scatter_progressive(DevCtx& c, uint8_t* host, const long long* pix, const uint32_t* patch,
@@ -438,24 +441,27 @@ int scatter_progressive(DevCtx& c, uint8_t* host, const long long* pix, const ui
   std::atomic<long long> next_query{0};
   const auto t0 = std::chrono::steady_clock::now();
   const size_t nblk = (ndep + kScatterBlock - 1) / kScatterBlock;
+  const size_t nch = (nblk + kScatterChunk - 1) / kScatterChunk;
+  // per block: entries consumed from its start; per chunk: 0 free, 1 held by a thread, 2 done
+  // (a chunk's cursors are read and written only by the thread holding it)
+  std::vector<uint8_t> cur(nblk, 0);
+  std::unique_ptr<std::atomic<int>[]> state(new std::atomic<int>[nch]);
+  for (size_t k = 0; k < nch; ++k) state[k].store(0, std::memory_order_relaxed);
   HostPool::get(c.device).run([&](int part, int parts) {
-    std::vector<size_t> pend;   // per pending block: its first unconsumed entry
-    pend.reserve(nblk / parts + 1);
-    const size_t per = (nblk + parts - 1) / parts;
-    for (size_t k = (size_t)part * per; k < nblk && k < (size_t)(part + 1) * per; ++k)
-      pend.push_back(k * kScatterBlock);
-    if (pend.empty()) return;
-    for (;;) {
-      const bool last = over.load(std::memory_order_acquire);
-      if (status.load(std::memory_order_relaxed) != (int)hipSuccess) return;
-      size_t got = 0, keep = 0;
-      for (size_t i = 0; i < pend.size(); ++i) {
-        size_t j = pend[i];
-        const size_t end = std::min((j / kScatterBlock + 1) * kScatterBlock, ndep);
+    const size_t per = (nch + parts - 1) / parts;
+    const size_t h0 = std::min((size_t)part * per, nch), h1 = std::min(h0 + per, nch);
+    // one chunk's ready entries; true once every entry is consumed (after the frame's end,
+    // `last`, an unmarked entry is passed over: it stays unmarked)
+    auto sweep = [&](size_t k, bool last, size_t& got) {
+      bool done = true;
+      const size_t bend = std::min((k + 1) * kScatterChunk, nblk);
+      for (size_t bl = k * kScatterChunk; bl < bend; ++bl) {
+        const size_t base = bl * kScatterBlock, end = std::min(base + kScatterBlock, ndep);
+        size_t j = base + cur[bl];
         for (; j < end; ++j) {
           const uint32_t v = *(const volatile uint32_t*)(patch + j);
           if ((v & 0xFF000000u) != mark) {
-            if (last) continue;   // after the frame an unmarked entry stays unmarked
+            if (last) continue;
             break;
           }
           uint8_t* q = host + 3 * (size_t)pix[j];
@@ -464,11 +470,38 @@ int scatter_progressive(DevCtx& c, uint8_t* host, const long long* pix, const ui
           q[2] = (uint8_t)(v >> 16);
           ++got;
         }
-        if (j < end) pend[keep++] = j;
+        cur[bl] = (uint8_t)(j - base);
+        if (j < end) done = false;
       }
-      pend.resize(keep);
-      if (pend.empty() || last) return;
-      if (got) continue;
+      return done;
+    };
+    for (;;) {
+      const bool last = over.load(std::memory_order_acquire);
+      if (status.load(std::memory_order_relaxed) != (int)hipSuccess) return;
+      size_t got = 0;
+      bool home_left = false, any_left = false;
+      // the thread's own chunks first (a band of rows: the caller's pixmap stays local); once
+      // they are all done, every other chunk not held by another thread, from the next
+      // thread's band on — the frame's last entries (the longest chains') sit in one or two
+      // bands, and every idle thread shares them
+      for (size_t i = 0; i < nch; ++i) {
+        const size_t k = (h0 + i) % nch;
+        const bool home = k >= h0 && k < h1;
+        if (!home && home_left && !last) break;
+        int st = state[k].load(std::memory_order_acquire);
+        if (st == 2) continue;
+        any_left = true;
+        if (home) home_left = true;
+        if (st != 0 || !state[k].compare_exchange_strong(st, 1, std::memory_order_acquire))
+          continue;
+        const bool done = sweep(k, last, got);
+        state[k].store(done ? 2 : 0, std::memory_order_release);
+      }
+      if (!any_left) return;
+      if (got || last) {
+        if (last) std::this_thread::yield();   // chunks another thread still holds
+        continue;
+      }
       const long long now = std::chrono::duration_cast<std::chrono::nanoseconds>(
                                 std::chrono::steady_clock::now() - t0).count();
       long long due = next_query.load(std::memory_order_relaxed);
