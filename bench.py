@@ -81,15 +81,15 @@ def load_pkg():
 # scripts/pmc_all.sh (kernel stats, VALU/wave-state and FETCH/WRITE passes per configuration ->
 # scripts/pmc_summary.py): per-kernel counter means per launch.  Lone frames for parity (the
 # one-frame-at-a-time schedule, phase C inside the resolver), the timed launches for fast mode.
-PMC_PROFILES = {("quadric", 4096, 6, "parity"): "profiles/r06g_pmc_c4.json",
-                ("reflection", 2048, 4, "parity"): "profiles/r06g_pmc_c3.json",
-                ("quadric", 8192, 6, "parity"): "profiles/r06g_pmc_c5.json",
-                ("quadric", 4096, 6, "fast"): "profiles/r06g_pmc_fast.json"}
+PMC_PROFILES = {("quadric", 4096, 6, "parity"): "profiles/r06s_pmc_c4.json",
+                ("reflection", 2048, 4, "parity"): "profiles/r06s_pmc_c3.json",
+                ("quadric", 8192, 6, "parity"): "profiles/r06s_pmc_c5.json",
+                ("quadric", 4096, 6, "fast"): "profiles/r06s_pmc_fast.json"}
 
 # The headline's whole counter set from the same call, on the driver's command itself
 # (`bench.py --timed-only --steps 20 --warmup 5`, frames in flight): valu_busy and traffic of
 # the headline line's dominant kernel come from the launches it times.
-PMC_HEADLINE = {("quadric", 4096, 6, "parity"): "profiles/r06g_pmc_headline.json"}
+PMC_HEADLINE = {("quadric", 4096, 6, "parity"): "profiles/r06s_pmc_headline.json"}
 
 
 def pmc_kernel(kernel, scene, size, depth, mode, inflight=False):

@@ -149,7 +149,7 @@ def test_counter_files_exist_and_are_current():
     maps = list(bench.PMC_PROFILES.items()) + list(bench.PMC_HEADLINE.items())
     assert maps
     for (scene, size, depth, mode), rel in maps:
-        assert os.path.basename(rel).startswith("r06g_"), rel
+        assert os.path.basename(rel).startswith("r06s_"), rel
         with open(os.path.join(ROOT, rel)) as f:
             ks = {k.split("::")[-1].split("<")[0] for k in json.load(f)["kernels"]}
         want = "k_render" if mode == "fast" else "k_resolve"
