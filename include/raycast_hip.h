@@ -214,6 +214,12 @@ int rc_lone_frames_check(int64_t *checked, int64_t *failed);
 /* Test aid: the nth_frame-th parity frame from now (0 = the next, any entry point, any
  * device) fails its hand-off as a timed-out spin would (error code 4); -1 cancels. */
 int rc_debug_inject_error(int nth_frame);
+/* Test aid (no GPU needed): rc_render's in-frame scatter of the mapped colour patch against a
+ * host thread standing in for phase C — ndep entries stored in shuffled batches, each batch in
+ * pieces, over an earlier frame's marks; skip != 0 leaves entries j % |skip| == 0 unstored,
+ * and skip < 0 then ends the frame with a failure (-2).  Returns the number of wrong pixmap bytes (0) or the
+ * sweep's failure status (< 0); -1 for ndep outside 1 .. 2^24. */
+int rc_debug_scatter_selftest(int64_t ndep, int64_t seed, int skip);
 /* Wait for every submitted frame, then release the current device's frame pipeline (its
  * CU-partitioned streams and events; the frame workspaces stay allocated).  The next
  * rc_frame_submit builds it again, re-reading RC_PIPE_* from the environment.  Returns what

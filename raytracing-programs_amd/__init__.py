@@ -136,7 +136,7 @@ HIP_EXPORTS = ["raycast", "rc_default_options", "rc_scene_create", "rc_scene_des
                "rc_group_transport", "rc_render_sharded", "rc_group_last_stats",
                "rc_default_tuning", "rc_set_tuning", "rc_get_tuning", "rc_lone_frames_check",
                "rc_debug_inject_error", "rc_group_debug_bound", "rc_resolver_stats_get",
-               "rc_group_rank_stats"]
+               "rc_group_rank_stats", "rc_debug_scatter_selftest"]
 FRONT_EXPORTS = ["add_new_sphere", "add_new_plane", "add_new_quadric", "free_shape_list",
                  "free_light_list", "add_new_spot_light", "add_new_point_light", "parse_json",
                  "set_to_black", "ppm_WriteOutP3", "ppm_clamp"]
@@ -471,6 +471,14 @@ def inject_error(nth_frame):
     fails its carry hand-off as a timed-out spin would; -1 cancels."""
     if hip_lib().rc_debug_inject_error(int(nth_frame)) != 0:
         raise ValueError(nth_frame)
+
+
+def scatter_selftest(ndep, seed=0, skip=0):
+    """Test aid (rc_debug_scatter_selftest, no GPU): rc_render's in-frame scatter against a
+    host writer thread; returns the number of wrong pixmap bytes or the failure status."""
+    lib = hip_lib()
+    lib.rc_debug_scatter_selftest.argtypes = [ctypes.c_int64, ctypes.c_int64, ctypes.c_int]
+    return lib.rc_debug_scatter_selftest(int(ndep), int(seed), int(skip))
 
 
 def write_p3(img, path):

@@ -9,6 +9,7 @@
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cmath>
@@ -19,6 +20,7 @@
 #include <functional>
 #include <memory>
 #include <mutex>
+#include <random>
 #include <string>
 #include <thread>
 #include <vector>
@@ -434,10 +436,13 @@ constexpr size_t kScatterBlock = 64;
 constexpr size_t kScatterChunk = 32;   // blocks per chunk: the unit a thread locks (2048 entries)
 constexpr long long kScatterQueryNs = 20000;
 
-int scatter_progressive(DevCtx& c, uint8_t* host, const long long* pix, const uint32_t* patch,
-                        size_t ndep, uint32_t mark, hipEvent_t ev_done) {
+// The sweep itself, on `pool`, with the frame's end as `probe()` (1 complete, 0 not yet, a
+// negative value a failure, returned as is); rc_debug_scatter_selftest drives it without a GPU.
+template <class Probe>
+int scatter_sweep(HostPool& pool, uint8_t* host, const long long* pix, const uint32_t* patch,
+                  size_t ndep, uint32_t mark, Probe probe) {
   std::atomic<bool> over{false};
-  std::atomic<int> status{(int)hipSuccess};
+  std::atomic<int> status{0};
   std::atomic<long long> next_query{0};
   const auto t0 = std::chrono::steady_clock::now();
   const size_t nblk = (ndep + kScatterBlock - 1) / kScatterBlock;
@@ -447,7 +452,7 @@ int scatter_progressive(DevCtx& c, uint8_t* host, const long long* pix, const ui
   std::vector<uint8_t> cur(nblk, 0);
   std::unique_ptr<std::atomic<int>[]> state(new std::atomic<int>[nch]);
   for (size_t k = 0; k < nch; ++k) state[k].store(0, std::memory_order_relaxed);
-  HostPool::get(c.device).run([&](int part, int parts) {
+  pool.run([&](int part, int parts) {
     const size_t per = (nch + parts - 1) / parts;
     const size_t h0 = std::min((size_t)part * per, nch), h1 = std::min(h0 + per, nch);
     // one chunk's ready entries; true once every entry is consumed (after the frame's end,
@@ -477,7 +482,7 @@ int scatter_progressive(DevCtx& c, uint8_t* host, const long long* pix, const ui
     };
     for (;;) {
       const bool last = over.load(std::memory_order_acquire);
-      if (status.load(std::memory_order_relaxed) != (int)hipSuccess) return;
+      if (status.load(std::memory_order_relaxed) != 0) return;
       size_t got = 0;
       bool home_left = false, any_left = false;
       // the thread's own chunks first (a band of rows: the caller's pixmap stays local); once
@@ -509,24 +514,32 @@ int scatter_progressive(DevCtx& c, uint8_t* host, const long long* pix, const ui
         std::this_thread::yield();
         continue;
       }
-      const hipError_t q = hipEventQuery(ev_done);
-      if (q == hipSuccess) {
+      const int q = probe();
+      if (q == 1) {
         over.store(true, std::memory_order_release);
-      } else if (q != hipErrorNotReady) {
-        status.store((int)q, std::memory_order_relaxed);
+      } else if (q != 0) {
+        status.store(q, std::memory_order_relaxed);
         return;
       } else {
         std::this_thread::yield();
       }
     }
   });
+  return status.load();
+}
+
+int scatter_progressive(DevCtx& c, uint8_t* host, const long long* pix, const uint32_t* patch,
+                        size_t ndep, uint32_t mark, hipEvent_t ev_done) {
+  const int st = scatter_sweep(HostPool::get(c.device), host, pix, patch, ndep, mark, [&] {
+    const hipError_t q = hipEventQuery(ev_done);
+    return q == hipSuccess ? 1 : q == hipErrorNotReady ? 0 : -(int)q;
+  });
   // a query's hipErrorNotReady is not a failure: clear it from this thread's last error (the
   // pool's threads keep theirs; nothing reads them)
   (void)hipGetLastError();
-  const int st = status.load();
-  if (st != (int)hipSuccess) {
+  if (st != 0) {
     std::fprintf(stderr, "Error: HIP call failed: hipEventQuery (%s) during the in-frame scatter\n",
-                 hipGetErrorString((hipError_t)st));
+                 hipGetErrorString((hipError_t)(-st)));
     return -1;
   }
   return 0;
@@ -1688,6 +1701,68 @@ int rc_debug_inject_error(int nth_frame) {
   if (nth_frame < -1) return -1;
   g_inject = nth_frame;
   return 0;
+}
+
+// Test aid: the in-frame scatter (scatter_sweep) on the host alone, a writer thread standing in
+// for phase C.  ndep DEP entries at increasing pixels (scan order); half the patch entries
+// start with an earlier frame's mark; the writer stores this frame's entries in shuffled
+// 64-entry batches, each batch's entries in a shuffled order (k_dep_chunks stores a batch in
+// pieces), with pauses, then reports the frame complete.  skip > 0: entries j % skip == 0 are
+// never stored (a frame that ended early: the sweep must still end, those pixels untouched);
+// skip < 0: entries j % -skip == 0 are never stored and the frame reports a failure instead of
+// completing.  Returns the number of pixmap bytes that differ from the expected image, or the
+// sweep's failure status (< 0).
+int rc_debug_scatter_selftest(int64_t ndep, int64_t seed, int skip) {
+  if (ndep <= 0 || ndep > ((int64_t)1 << 24)) return -1;
+  const size_t n = (size_t)ndep;
+  std::mt19937_64 rng((uint64_t)seed);
+  const size_t gap = skip > 0 ? (size_t)skip : skip < 0 ? (size_t)-(int64_t)skip : 0;
+  std::vector<long long> pix(n);
+  long long p = 0;
+  for (size_t j = 0; j < n; ++j) {
+    p += 1 + (long long)(rng() % 3);
+    pix[j] = p;
+  }
+  std::vector<uint8_t> host(3 * ((size_t)p + 1), 0), want(host.size(), 0);
+  std::vector<uint32_t> patch(n), colour(n);
+  const uint32_t mark = rc::patch_mark(7), stale = rc::patch_mark(6);
+  for (size_t j = 0; j < n; ++j) {
+    colour[j] = (uint32_t)rng() & 0xFFFFFFu;
+    patch[j] = (rng() & 1) ? (stale | ((uint32_t)rng() & 0xFFFFFFu)) : 0u;
+    if (gap && j % gap == 0) continue;
+    uint8_t* q = want.data() + 3 * (size_t)pix[j];
+    q[0] = (uint8_t)colour[j];
+    q[1] = (uint8_t)(colour[j] >> 8);
+    q[2] = (uint8_t)(colour[j] >> 16);
+  }
+  const size_t nb = (n + kScatterBlock - 1) / kScatterBlock;
+  std::vector<size_t> order(nb);
+  for (size_t b = 0; b < nb; ++b) order[b] = b;
+  std::shuffle(order.begin(), order.end(), rng);
+  std::atomic<int> done{0};
+  std::thread writer([&] {
+    std::mt19937_64 wr((uint64_t)seed + 1);
+    size_t idx[kScatterBlock];
+    for (size_t i = 0; i < nb; ++i) {
+      const size_t b0 = order[i] * kScatterBlock, cnt = std::min(kScatterBlock, n - b0);
+      for (size_t k = 0; k < cnt; ++k) idx[k] = b0 + k;
+      std::shuffle(idx, idx + cnt, wr);
+      for (size_t k = 0; k < cnt; ++k) {
+        const size_t j = idx[k];
+        if (gap && j % gap == 0) continue;
+        __atomic_store_n(&patch[j], mark | colour[j], __ATOMIC_RELEASE);
+      }
+      if (wr() % 8 == 0) std::this_thread::sleep_for(std::chrono::microseconds(wr() % 40));
+    }
+    done.store(skip < 0 ? -2 : 1, std::memory_order_release);
+  });
+  const int st = scatter_sweep(HostPool::get(0), host.data(), pix.data(), patch.data(), n, mark,
+                               [&] { return done.load(std::memory_order_acquire); });
+  writer.join();
+  if (st != 0) return st;
+  long long bad = 0;
+  for (size_t i = 0; i < host.size(); ++i) bad += host[i] != want[i];
+  return (int)std::min<long long>(bad, 1 << 30);
 }
 
 int rc_profile_begin(void) {
