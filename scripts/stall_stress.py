@@ -3,6 +3,7 @@ estimate how often a resolver hand-off times out (the frame then fails loudly). 
 first failure of each schedule.  With RC_STRESS_FLIGHT=1 the frames go in flight instead
 (rc_frame_submit into 8 rotating buffers, rc_frames_wait every 40 frames; the last 8 frames'
 bytes checked against the first frame's).
+SCENE / SIZE / DEPTH pick another configuration (default quadric 4096 6).
 Usage: [RC_STRESS_FLIGHT=1] python scripts/stall_stress.py FRAMES [name:k=v,k=v ...]"""
 import importlib.util
 import os
@@ -23,8 +24,10 @@ scheds = []
 for a in sys.argv[2:] or ["default:"]:
     name, _, kv = a.partition(":")
     scheds.append((name, {k: int(v) for k, v in (p.split("=") for p in kv.split(",") if p)}))
-scene = pkg.Scene.from_file(os.path.join(ROOT, "tests", "golden", "scenes", "quadric.scene"))
-W = H = 4096
+scene = pkg.Scene.from_file(os.path.join(ROOT, "tests", "golden", "scenes",
+                                        os.environ.get("SCENE", "quadric") + ".scene"))
+W = H = int(os.environ.get("SIZE", "4096"))
+D = int(os.environ.get("DEPTH", "6"))
 out = torch.empty((H, W, 3), dtype=torch.uint8, device="cuda:0")
 flight = os.environ.get("RC_STRESS_FLIGHT") == "1"
 bufs = [torch.empty((H, W, 3), dtype=torch.uint8, device="cuda:0") for _ in range(8 if flight else 0)]
@@ -35,7 +38,7 @@ for name, tune in scheds:
         for i in range(frames):
             try:
                 if flight:
-                    pkg.frame_submit(scene, W, H, bufs[i % 8].data_ptr())
+                    pkg.frame_submit(scene, W, H, bufs[i % 8].data_ptr(), depth=D)
                     if i % 40 == 39 or i == frames - 1:
                         pkg.frames_wait()
                         if i == frames - 1:
@@ -44,7 +47,7 @@ for name, tune in scheds:
                             if same != len(bufs):
                                 raise RuntimeError(f"only {same} of {len(bufs)} buffers equal")
                 else:
-                    pkg.render_device(scene, W, H, out.data_ptr())
+                    pkg.render_device(scene, W, H, out.data_ptr(), depth=D)
                     torch.cuda.synchronize()
                     if pkg.lone_frames_check()["failed"]:
                         raise RuntimeError("lone_frames_check reports a failed frame")
