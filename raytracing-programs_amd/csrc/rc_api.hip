@@ -387,9 +387,10 @@ int ensure_pinned(DevCtx& c, size_t entries) {
 // frame's mark (rc::patch_mark of the frame's epoch) and the host never stores to the array
 // while a frame runs: a frame's entries are known by the mark alone.  Marks repeat every
 // rc::kPatchMarks epochs, so before a frame of epoch `epoch` is enqueued the array's possibly
-// marked entries (host_patch_dirty) are cleared once `epoch` is that far past the last clear.  rc_render
-// raises host_patch_dirty to the whole image before it enqueues a frame that writes the array
-// and lowers it to the largest DEP count since the clear once the frame's own is known.
+// marked entries (host_patch_dirty) are cleared once `epoch` is that far past the last clear.
+// rc_render raises host_patch_dirty to the whole image before it enqueues a frame that writes
+// the array and lowers it to the largest DEP count since the clear once the frame's own is
+// known.
 int ensure_host_patch(DevCtx& c, size_t entries, unsigned epoch) {
   if (entries <= c.host_patch_entries) {
     if (c.host_patch_dirty &&
@@ -428,10 +429,10 @@ int ensure_host_patch(DevCtx& c, size_t entries, unsigned epoch) {
 // sweeps its own band of chunks (contiguous, so its pixels are a band of rows: spreading every
 // thread over the whole image made the scatter ~5x slower per entry, TLB and cache misses on
 // the caller's pixmap, profiles/r06n_scatter_diag.txt) and, once its band is done, helps with
-// the others'.  A sweep that found nothing yields; the event is
-// queried by one thread at a time, at most once per kScatterQueryNs (every thread querying
-// after each short sweep contends in the runtime); any status other than "not ready" ends
-// every thread's sweeps (the frame failed: returns -1, the caller reports it).
+// the others'.  A sweep that found nothing yields; the event is queried by one thread at a
+// time, at most once per kScatterQueryNs (every thread querying after each short sweep
+// contends in the runtime); any status other than "not ready" ends every thread's sweeps (the
+// frame failed: returns -1, the caller reports it).
 constexpr size_t kScatterBlock = 64;
 constexpr size_t kScatterChunk = 32;   // blocks per chunk: the unit a thread locks (2048 entries)
 constexpr long long kScatterQueryNs = 20000;
