@@ -429,13 +429,17 @@ int ensure_host_patch(DevCtx& c, size_t entries, unsigned epoch) {
 // sweeps its own band of chunks (contiguous, so its pixels are a band of rows: spreading every
 // thread over the whole image made the scatter ~5x slower per entry, TLB and cache misses on
 // the caller's pixmap, profiles/r06n_scatter_diag.txt) and, once its band is done, helps with
-// the others'.  A sweep that found nothing yields; the event is queried by one thread at a
+// the others' (frames of kScatterHelpMin entries or more).  A sweep that found nothing yields; the event is queried by one thread at a
 // time, at most once per kScatterQueryNs (every thread querying after each short sweep
 // contends in the runtime); any status other than "not ready" ends every thread's sweeps (the
 // frame failed: returns -1, the caller reports it).
 constexpr size_t kScatterBlock = 64;
 constexpr size_t kScatterChunk = 32;   // blocks per chunk: the unit a thread locks (2048 entries)
 constexpr long long kScatterQueryNs = 20000;
+// below this many entries a thread sweeps its own band only: helping costs ~1 % end to end on
+// frames whose scatter is short (reflection 2048^2 d4, 0.29 M entries; simple 1024^2 d6) and
+// saves 0.04-0.1 ms at quadric 4096^2 (2.8 M; profiles/r06y_scatter_help_ab.txt)
+constexpr size_t kScatterHelpMin = (size_t)1 << 20;
 
 // The sweep itself, on `pool`, with the frame's end as `probe()` (1 complete, 0 not yet, a
 // negative value a failure, returned as is); rc_debug_scatter_selftest drives it without a GPU.
@@ -453,9 +457,11 @@ int scatter_sweep(HostPool& pool, uint8_t* host, const long long* pix, const uin
   std::vector<uint8_t> cur(nblk, 0);
   std::unique_ptr<std::atomic<int>[]> state(new std::atomic<int>[nch]);
   for (size_t k = 0; k < nch; ++k) state[k].store(0, std::memory_order_relaxed);
+  const bool help = ndep >= kScatterHelpMin;
   pool.run([&](int part, int parts) {
     const size_t per = (nch + parts - 1) / parts;
     const size_t h0 = std::min((size_t)part * per, nch), h1 = std::min(h0 + per, nch);
+    const size_t span = help ? nch : h1 - h0;
     // one chunk's ready entries; true once every entry is consumed (after the frame's end,
     // `last`, an unmarked entry is passed over: it stays unmarked)
     auto sweep = [&](size_t k, bool last, size_t& got) {
@@ -490,7 +496,7 @@ int scatter_sweep(HostPool& pool, uint8_t* host, const long long* pix, const uin
       // they are all done, every other chunk not held by another thread, from the next
       // thread's band on — the frame's last entries (the longest chains') sit in one or two
       // bands, and every idle thread shares them
-      for (size_t i = 0; i < nch; ++i) {
+      for (size_t i = 0; i < span; ++i) {
         const size_t k = (h0 + i) % nch;
         const bool home = k >= h0 && k < h1;
         if (!home && home_left && !last) break;
