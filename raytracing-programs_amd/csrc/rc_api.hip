@@ -1087,6 +1087,33 @@ int report_spin_error(const FrameBufs& b, const char* where) {
                "prod %d claim %d finished %d, side workgroups go %d gave-up %d\n",
                e[0], spin_site(e[0]), where, e[1], e[2], e[3], cnt[0],
                cnt[2], cnt[5], dq[0], dq[1], dq[2], cnt[12], cnt[13]);
+  if (e[0] == 1) {   // a team hand-off: each team block's latest published round (its slots)
+    const int nb = rc::team_slot_bufs(), nt = rc::team_slot_blocks();
+    std::vector<unsigned long long> sl((size_t)nb * nt * 4);
+    if (hipMemcpy(sl.data(), (const char*)b.team.p + rc::team_slot_offset(),
+                  sl.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost) == hipSuccess) {
+      std::vector<int> last(nt, 0);   // the latest round whose four granules all arrived
+      for (int q = 0; q < nb; ++q)
+        for (int k = 0; k < nt; ++k) {
+          int r = 1 << 30;
+          for (int g = 0; g < 4; ++g)
+            r = std::min(r, (int)(unsigned)(sl[((size_t)q * nt + k) * 4 + g] >> 32));
+          last[k] = std::max(last[k], r);
+        }
+      int lo = 1 << 30, hi = 0;
+      for (int k = 0; k < nt; ++k)
+        if (last[k] > 0) lo = std::min(lo, last[k]), hi = std::max(hi, last[k]);
+      std::fprintf(stderr, "  team slots: latest round per block %d .. %d; behind:", lo, hi);
+      int shown = 0;
+      for (int k = 0; k < nt && shown < 16; ++k)
+        if (last[k] > 0 && last[k] < hi) std::fprintf(stderr, " %d:%d", k, last[k]), ++shown;
+      std::fprintf(stderr, "\n  slot[round %% %d][block %d] tags:", nb, e[3]);
+      for (int q = 0; q < nb && e[3] >= 0 && e[3] < nt; ++q)
+        for (int g = 0; g < 4; ++g)
+          std::fprintf(stderr, " %u", (unsigned)(sl[((size_t)q * nt + e[3]) * 4 + g] >> 32));
+      std::fprintf(stderr, "\n");
+    }
+  }
   const int nseg = cnt[0], ndep = cnt[2];
   if (nseg > 0 && ndep > 0 && b.cin.p && b.seg_start.p) {
     std::vector<int> starts(nseg);
@@ -1683,6 +1710,9 @@ int rc_lone_frames_check(int64_t* checked, int64_t* failed) {
   c->lone_log.take(&ch, &f);
   if (checked) *checked = ch;
   if (failed) *failed = f;
+  // the details of the device workspace's last frame (the failed one when the caller checks
+  // after each frame): the spin that failed, the helper queue, the team's slots
+  if (f && c->fb.team.p) (void)report_spin_error(c->fb, "the device workspace's last frame");
   return f ? -1 : 0;
 }
 

@@ -148,6 +148,9 @@ size_t deprec_bytes();
 size_t row_stats_bytes();
 size_t team_state_bytes();
 size_t team_dq_offset();   // DenseQueue {prod, claim, finished} inside TeamState
+size_t team_slot_offset(); // the team's hand-off slots: [team_slot_bufs()][team_slot_blocks()]
+int team_slot_bufs();      //   x 4 tagged granules {payload, round}
+int team_slot_blocks();
 int resolve_blocks_resident(int cus, int lds_bytes);
 // k_resolve<true>'s resources: registers per lane (VGPRs + AGPRs), scratch bytes per lane, and
 // the workgroups one CU can hold with `lds_bytes` of dynamic LDS each (occupancy API).

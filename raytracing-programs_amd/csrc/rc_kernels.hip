@@ -1478,10 +1478,12 @@ __device__ __forceinline__ int block_window(const Scene& sc, int maxrec, BlockWi
 // publishes, every block collects it), and RESOLVE rounds never follow each other.  So while
 // a slow block still reads round r, the others can publish at most up to round r + 2: after
 // a SCAN round r, a RESOLVE round r + 1 waits for nobody but block 0, and the SCAN round r + 2
-// cannot be collected without the slow block's own publish.  Round parity (two buffers) let
-// round r + 2 overwrite a round-r slot still unread: the reader then spun out its 5 s limit
-// on a tag it would never see (1 frame in ~200-300 with split shading, whose k_side work slows
-// the team's collects; profiles/r06o_team_slot_race.txt).
+// cannot be collected without the slow block's own publish.  With round parity (two buffers)
+// a hand-off spun out its 5 s limit in 1 frame of ~200-300 with split shading, whose k_side
+// work slows the team; rotating over four rounds brought that to ~1 in 5 000-14 000
+// (profiles/r06o_team_slot_race.txt).  The residual failure is not an overwrite: every other
+// block waits for block 0's RESOLVE round r while block 0's slot holds r and r + 1 when the
+// frame ends (profiles/r06zz_split_shade_residual.txt; open, split shading only).
 constexpr int kTeamBufs = 4;
 struct alignas(32) TeamSlot {
   unsigned long long g[4];
@@ -3119,6 +3121,9 @@ static void enqueue_phase_c(const Scene& sc, const Cam& cam, bool st, int W, int
 
 size_t team_state_bytes() { return sizeof(TeamState); }
 size_t team_dq_offset() { return offsetof(TeamState, dq); }
+size_t team_slot_offset() { return offsetof(TeamState, slot); }
+int team_slot_bufs() { return kTeamBufs; }
+int team_slot_blocks() { return kTeamMax; }
 
 // k_side workgroups per CU such that one resolver workgroup (one wave per SIMD) still fits
 // beside them in every SIMD's 512 VGPRs: k_side waits for the resolver's census, so it must

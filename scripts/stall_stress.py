@@ -3,7 +3,8 @@ estimate how often a resolver hand-off times out (the frame then fails loudly). 
 first failure of each schedule.  With RC_STRESS_FLIGHT=1 the frames go in flight instead
 (rc_frame_submit into 8 rotating buffers, rc_frames_wait every 40 frames; the last 8 frames'
 bytes checked against the first frame's).
-SCENE / SIZE / DEPTH pick another configuration (default quadric 4096 6).
+SCENE / SIZE / DEPTH pick another configuration (default quadric 4096 6); RC_STRESS_HOST=1
+renders through rc_render (whose failure report includes the resolver's state).
 Usage: [RC_STRESS_FLIGHT=1] python scripts/stall_stress.py FRAMES [name:k=v,k=v ...]"""
 import importlib.util
 import os
@@ -46,6 +47,8 @@ for name, tune in scheds:
                             same = sum(1 for b in bufs if torch.equal(b, ref))
                             if same != len(bufs):
                                 raise RuntimeError(f"only {same} of {len(bufs)} buffers equal")
+                elif os.environ.get("RC_STRESS_HOST") == "1":   # rc_render: a failure's details on stderr
+                    pkg.render(scene, W, H, depth=D)
                 else:
                     pkg.render_device(scene, W, H, out.data_ptr(), depth=D)
                     torch.cuda.synchronize()
