@@ -1113,6 +1113,20 @@ int report_spin_error(const FrameBufs& b, const char* where) {
           std::fprintf(stderr, " %u", (unsigned)(sl[((size_t)q * nt + e[3]) * 4 + g] >> 32));
       std::fprintf(stderr, "\n");
     }
+    if (const size_t off = rc::team_handoff_diag_offset()) {   // RC_HANDOFF_DIAG builds
+      unsigned long long t[1 + 4] = {};
+      int r[4] = {};
+      const int nb = std::min(rc::team_slot_bufs(), 4);
+      if (hipMemcpy(t, (const char*)b.team.p + off, sizeof(unsigned long long) * (1 + nb),
+                    hipMemcpyDeviceToHost) == hipSuccess &&
+          hipMemcpy(r, (const char*)b.team.p + off + sizeof(unsigned long long) * (1 + nb),
+                    sizeof(int) * nb, hipMemcpyDeviceToHost) == hipSuccess) {
+        std::fprintf(stderr, "  block 0 published (round: us relative to the first failed spin):");
+        for (int q = 0; q < nb; ++q)
+          std::fprintf(stderr, " %d: %.1f", r[q], ((double)t[1 + q] - (double)t[0]) / 100.0);
+        std::fprintf(stderr, "\n");
+      }
+    }
   }
   const int nseg = cnt[0], ndep = cnt[2];
   if (nseg > 0 && ndep > 0 && b.cin.p && b.seg_start.p) {

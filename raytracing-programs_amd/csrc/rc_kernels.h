@@ -151,6 +151,7 @@ size_t team_dq_offset();   // DenseQueue {prod, claim, finished} inside TeamStat
 size_t team_slot_offset(); // the team's hand-off slots: [team_slot_bufs()][team_slot_blocks()]
 int team_slot_bufs();      //   x 4 tagged granules {payload, round}
 int team_slot_blocks();
+size_t team_handoff_diag_offset();   // 0 unless an RC_HANDOFF_DIAG build
 int resolve_blocks_resident(int cus, int lds_bytes);
 // k_resolve<true>'s resources: registers per lane (VGPRs + AGPRs), scratch bytes per lane, and
 // the workgroups one CU can hold with `lds_bytes` of dynamic LDS each (occupancy API).

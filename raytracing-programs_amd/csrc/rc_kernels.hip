@@ -769,6 +769,9 @@ __global__ void __launch_bounds__(256) k_row_compact(
 // team_blocks*256-entry window per round and agree on the first changer through a counter
 // barrier (all team blocks are co-resident: they are the first blocks of a grid sized to the
 // device's resident capacity).
+#ifndef RC_HANDOFF_DIAG
+#define RC_HANDOFF_DIAG 0   // 1: experiment builds record block 0's publish times (TeamState)
+#endif
 #ifndef RC_DIAG
 #define RC_DIAG 0   // 1: the diagnostic builds (make stamps / stamps2) write the resolver trace
 #endif
@@ -1536,6 +1539,12 @@ struct TeamState {
   int pad[16];
   TeamSlot slot[kTeamBufs][kTeamMax];
   DenseQueue dq;
+#if RC_HANDOFF_DIAG   // experiment builds: when the first spin failed, when block 0 published
+  unsigned long long hd_err_t;
+  unsigned long long hd_pub_t[kTeamBufs];
+  int hd_pub_round[kTeamBufs];
+  int hd_pad[2];
+#endif
 };
 
 static_assert(sizeof(TeamState) % 16 == 0, "k_row_stats clears TeamState in 16-byte words");
@@ -1553,6 +1562,10 @@ __device__ __forceinline__ void set_error(TeamState* ts, int code, int info, int
   int expect = 0;
   if (__hip_atomic_compare_exchange_strong(&ts->error, &expect, code, __ATOMIC_RELAXED,
                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+#if RC_HANDOFF_DIAG
+    __hip_atomic_store(&ts->hd_err_t, (unsigned long long)__builtin_amdgcn_s_memrealtime(),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
     __hip_atomic_store(&ts->err_block, (int)blockIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(&ts->err_info, info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(&ts->err_info2, info2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1615,6 +1628,15 @@ __device__ __forceinline__ void ready_range(int* __restrict__ cnt, int* __restri
 
 __device__ __forceinline__ void team_publish(TeamState* ts, int round, unsigned pos, V3 c) {
   TeamSlot* sl = &ts->slot[round & (kTeamBufs - 1)][blockIdx.x];
+#if RC_HANDOFF_DIAG
+  if (blockIdx.x == 0) {
+    __hip_atomic_store(&ts->hd_pub_t[round & (kTeamBufs - 1)],
+                       (unsigned long long)__builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&ts->hd_pub_round[round & (kTeamBufs - 1)], round, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
+#endif
   const unsigned tag = (unsigned)round;
   __hip_atomic_store(&sl->g[0], pack2(pos, tag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __hip_atomic_store(&sl->g[1], pack2(__float_as_uint(c.x), tag), __ATOMIC_RELAXED,
@@ -3124,6 +3146,13 @@ size_t team_dq_offset() { return offsetof(TeamState, dq); }
 size_t team_slot_offset() { return offsetof(TeamState, slot); }
 int team_slot_bufs() { return kTeamBufs; }
 int team_slot_blocks() { return kTeamMax; }
+size_t team_handoff_diag_offset() {
+#if RC_HANDOFF_DIAG
+  return offsetof(TeamState, hd_err_t);
+#else
+  return 0;
+#endif
+}
 
 // k_side workgroups per CU such that one resolver workgroup (one wave per SIMD) still fits
 // beside them in every SIMD's 512 VGPRs: k_side waits for the resolver's census, so it must
